@@ -1,0 +1,44 @@
+"""Data sources: synthetic on-device tokens, native memmap shards, HF datasets (reference path)."""
+from .synthetic import SyntheticTokens
+
+
+def build_data(kind: str, *, vocab_size: int, seq_len: int, batch_size: int, seed: int, rank: int,
+               world_size: int, device, dataset_path: str = None, tokenizer: str = "huggyllama/llama-7b",
+               mask_pad_labels: bool = True):
+    if kind == "synthetic":
+        return SyntheticTokens(vocab_size, seq_len, batch_size, seed, rank, device)
+    if kind == "memmap":
+        import glob
+        import os
+
+        from .memmap import MemmapTokens
+        paths = sorted(glob.glob(os.path.join(dataset_path, "*.bin"))) if os.path.isdir(dataset_path) \
+            else sorted(glob.glob(dataset_path))
+        if not paths:
+            raise FileNotFoundError(f"no token shards at {dataset_path}")
+        return MemmapTokens(paths, seq_len, batch_size, vocab_size, seed, rank, world_size, device=device)
+    if kind == "hf":
+        from .hf import make_hf_loader
+        return _DeviceIter(make_hf_loader(dataset_path, tokenizer, seq_len, batch_size, world_size, rank, seed,
+                                          mask_pad_labels), device)
+    raise ValueError(f"unknown data source {kind}")
+
+
+class _DeviceIter:
+    def __init__(self, loader, device):
+        self.loader, self.device = loader, device
+        self._it = iter(loader)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        try:
+            b = next(self._it)
+        except StopIteration:  # epoch boundary: keep going (trainer is bounded by total_steps)
+            self._it = iter(self.loader)
+            b = next(self._it)
+        return {k: v.to(self.device, non_blocking=True) for k, v in b.items()}
+
+
+__all__ = ["SyntheticTokens", "build_data"]

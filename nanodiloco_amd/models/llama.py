@@ -1,0 +1,186 @@
+"""Llama causal LM over a flat :class:`ParamStore`.
+
+Architecture and parameter names/shapes are exactly HF ``LlamaForCausalLM``
+(HF/models/llama/modeling_llama.py:52-492), so checkpoints load into HF and HF
+weights load here.  The compute graph is our own:
+
+  h0  = embed(ids)                          fp32 residual stream, gathered from the fp32 master
+  y   = rmsnorm(h0) * w_in[0]               compute dtype (bf16)
+  per layer:
+    qkv = y @ [Wq|Wk|Wv]^T                  ONE GEMM (fused view of the flat buffer)
+    o   = flash_attn(rope(qkv))             HIP kernel, reads packed qkv, writes [N, nh*hd]
+    y,h = add_rmsnorm(h, o @ Wo^T, w_post)  residual add fused into the norm
+    gu  = y @ [Wgate|Wup]^T                 ONE GEMM
+    y,h = add_rmsnorm(h, swiglu(gu) @ Wdown^T, w_in[i+1] or w_final)
+  loss = lm_head_ce(y, W_lm, targets)       fused chunked GEMM + CE (+ its backward)
+
+Weight gradients are written straight into ``store.grad`` by the ops' backward (and, for the
+lm head, during the forward).  ``layer_hook`` lets the trainer react as soon as a layer's
+gradients are final (used for the inner-DDP bucketed all-reduce overlapped with backward).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Callable, List, Optional
+
+import torch
+
+from .. import ops
+from ..config import LlamaConfig
+from .param_store import ParamStore
+
+
+@dataclasses.dataclass
+class CausalLMOutput:
+    loss: Optional[torch.Tensor] = None
+    logits: Optional[torch.Tensor] = None
+
+
+class _GradHook(torch.autograd.Function):
+    """Identity; calls ``fn(idx)`` when the gradient w.r.t. its input has been produced."""
+
+    @staticmethod
+    def forward(ctx, x, fn, idx):
+        ctx.fn, ctx.idx = fn, idx
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.fn(ctx.idx)
+        return g, None, None
+
+
+class LlamaForCausalLM:
+    def __init__(self, config: LlamaConfig, device="cpu", compute_dtype: torch.dtype = torch.float32,
+                 store: Optional[ParamStore] = None, activation_checkpointing: bool = False):
+        self.config = config
+        self.device = torch.device(device)
+        self.compute_dtype = compute_dtype
+        self.activation_checkpointing = activation_checkpointing
+        L = config.num_hidden_layers
+        groups = []
+        for i in range(L):
+            p = f"model.layers.{i}."
+            groups.append([p + "self_attn.q_proj.weight", p + "self_attn.k_proj.weight", p + "self_attn.v_proj.weight"])
+            groups.append([p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight"])
+        self.store = store or ParamStore(config.param_shapes(), device, compute_dtype, fuse_groups=groups)
+        self._qkv_names = [g for g in groups[0::2]]
+        self._gu_names = [g for g in groups[1::2]]
+        self.layer_hook: Optional[Callable[[int], None]] = None
+        self.training = True
+
+    # ------------------------------------------------------------------ init / io
+    @torch.no_grad()
+    def init_weights(self, seed: int = 1337):
+        """HF ``_init_weights``: N(0, initializer_range) for Linear/Embedding, ones for RMSNorm."""
+        std = self.config.initializer_range
+        gen_dev = self.device if self.device.type == "cuda" else torch.device("cpu")
+        g = torch.Generator(device=gen_dev)
+        g.manual_seed(seed)
+        for name in self.store.names:
+            v = self.store.master_view(name)
+            if v.dim() == 1:
+                v.fill_(1.0)
+            else:
+                t = torch.empty(v.shape, dtype=torch.float32, device=gen_dev)
+                t.normal_(0.0, std, generator=g)
+                v.copy_(t)
+        pad = self.config.pad_token_id
+        if pad is not None:
+            self.store.master_view("model.embed_tokens.weight")[pad].zero_()
+        self.store.sync_shadow()
+        return self
+
+    def state_dict(self):
+        return self.store.state_dict("master")
+
+    def load_state_dict(self, sd, strict=True):
+        self.store.load_state_dict(sd, strict=strict)
+
+    def num_parameters(self) -> int:
+        return self.store.num_params
+
+    def train(self):
+        self.training = True
+        return self
+
+    def eval(self):
+        self.training = False
+        return self
+
+    def __call__(self, *a, **kw):
+        return self.forward(*a, **kw)
+
+    # ------------------------------------------------------------------ views
+    def _w(self, name):  # compute-dtype weight (GEMM operand)
+        return self.store.shadow_view(name)
+
+    def _m(self, name):  # fp32 master weight (norms, embedding gather)
+        return self.store.master_view(name)
+
+    def _g(self, name):
+        return self.store.grad_view(name) if self.training else None
+
+    def _fused(self, names, which):
+        if which == "grad" and not self.training:
+            return None
+        return self.store.fused_view(which, names)
+
+    # ------------------------------------------------------------------ forward
+    def _layer(self, i, h, y, cos, sin, B, T, next_norm):
+        c = self.config
+        p = f"model.layers.{i}."
+        cdt = self.compute_dtype
+        eps = c.rms_norm_eps
+        qn = self._qkv_names[i]
+        qkv = ops.linear(y, self._fused(qn, "shadow"), self._fused(qn, "grad"))
+        o = ops.attention(qkv, cos, sin, B, T, c.num_attention_heads, c.num_key_value_heads, c.head_dim)
+        a = ops.linear(o, self._w(p + "self_attn.o_proj.weight"), self._g(p + "self_attn.o_proj.weight"))
+        y, h = ops.add_rmsnorm(h, a, self._m(p + "post_attention_layernorm.weight"),
+                               self._g(p + "post_attention_layernorm.weight"), eps, cdt)
+        gn = self._gu_names[i]
+        gu = ops.linear(y, self._fused(gn, "shadow"), self._fused(gn, "grad"))
+        act = ops.swiglu(gu)
+        m = ops.linear(act, self._w(p + "mlp.down_proj.weight"), self._g(p + "mlp.down_proj.weight"))
+        return m, h
+
+    def hidden_states(self, input_ids: torch.Tensor) -> torch.Tensor:
+        """Final-normed hidden states [B*T, d] in the compute dtype."""
+        c = self.config
+        B, T = input_ids.shape
+        cdt = self.compute_dtype
+        eps = c.rms_norm_eps
+        cos, sin = ops.rope_cache(T, c.head_dim, c.rope_theta, c.rope_scaling, self.device)
+        h = ops.embedding(input_ids, self._m("model.embed_tokens.weight"), self._g("model.embed_tokens.weight"))
+        y = ops.rmsnorm(h, self._m("model.layers.0.input_layernorm.weight"),
+                        self._g("model.layers.0.input_layernorm.weight"), eps, cdt)
+        L = c.num_hidden_layers
+        for i in range(L):
+            nxt = f"model.layers.{i + 1}.input_layernorm.weight" if i + 1 < L else "model.norm.weight"
+            if self.activation_checkpointing and self.training and torch.is_grad_enabled():
+                from torch.utils.checkpoint import checkpoint
+                m, h = checkpoint(self._layer, i, h, y, cos, sin, B, T, nxt, use_reentrant=False)
+            else:
+                m, h = self._layer(i, h, y, cos, sin, B, T, nxt)
+            if self.layer_hook is not None and torch.is_grad_enabled():
+                h = _GradHook.apply(h, self.layer_hook, i)
+            y, h = ops.add_rmsnorm(h, m, self._m(nxt), self._g(nxt), eps, cdt)
+        return y
+
+    def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None, attention_mask=None,
+                loss_scale: float = 1.0, return_logits: bool = False, targets: Optional[torch.Tensor] = None
+                ) -> CausalLMOutput:
+        """``labels`` follow HF semantics (shifted internally, -100 ignored); ``attention_mask`` is
+        accepted for API parity: padded positions must be given label -100 by the caller."""
+        y = self.hidden_states(input_ids)
+        lm = "lm_head.weight" if not self.config.tie_word_embeddings else "model.embed_tokens.weight"
+        out = CausalLMOutput()
+        if labels is not None or targets is not None:
+            if targets is None:
+                targets = ops.reference.shift_labels(labels, ops.IGNORE_INDEX)
+            out.loss = ops.lm_head_ce(y, self._w(lm), self._g(lm), targets.reshape(-1), loss_scale)
+        if return_logits or (labels is None and targets is None):
+            with torch.no_grad():
+                B, T = input_ids.shape
+                out.logits = torch.mm(y.detach(), self._w(lm).t()).float().view(B, T, -1)
+        return out

@@ -1,0 +1,92 @@
+"""RoPE + causal flash attention on the packed QKV GEMM output (K4 + K6).
+
+Input ``qkv`` is the fused q|k|v projection output ``[B*T, (nh + 2*nkv) * hd]`` (token-major, heads
+packed).  The HIP path never transposes to ``[B, H, T, hd]``: the attention kernels take
+(batch, head, token) strides and read 128-B head rows straight out of the packed buffer, and
+write ``O`` as ``[B*T, nh*hd]`` -- exactly the o_proj GEMM input.
+
+HIP path
+  fwd: ``nd_rope_inplace`` on a copy of q|k (half-split rotation, fp32 tables)
+       ``nd_attn_fwd``  -- MFMA flash attention, online softmax, saves LSE (fp32, log2 domain)
+  bwd: ``nd_attn_bwd_pre`` (delta = rowsum(dO * O)), ``nd_attn_bwd`` (dQ, dK, dV; recomputes P from
+       LSE), ``nd_rope_inplace(inverse)`` on dq|dk.
+GQA (nkv < nh) is handled by head-index mapping inside the kernels (no K/V repetition).
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import torch
+
+from . import _ext
+from . import reference as ref
+
+_TABLES: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
+
+
+def rope_cache(T: int, hd: int, theta: float, scaling, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    key = (T, hd, float(theta), repr(scaling), str(device))
+    t = _TABLES.get(key)
+    if t is None:
+        cos, sin = ref.rope_tables(T, hd, theta, scaling, device="cpu")
+        t = (cos.to(device).contiguous(), sin.to(device).contiguous())
+        _TABLES[key] = t
+    return t
+
+
+def _rope(qkv, cos, sin, B, T, nh, nkv, hd, inverse):
+    L = _ext.lib()
+    _ext.check(L.nd_rope_inplace(_ext.ptr(qkv), _ext.dtcode(qkv), _ext.ptr(cos), _ext.ptr(sin), B * T, T,
+                                 nh, nkv, hd, qkv.shape[1], 1 if inverse else 0, _ext.stream_ptr(qkv.device)),
+               "nd_rope_inplace")
+
+
+class FlashAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, B, T, nh, nkv, hd):
+        qkv_r = qkv.clone()
+        _rope(qkv_r, cos, sin, B, T, nh, nkv, hd, inverse=False)
+        ld = qkv_r.shape[1]
+        q = qkv_r
+        k = qkv_r[:, nh * hd:]
+        v = qkv_r[:, (nh + nkv) * hd:]
+        o = torch.empty(B * T, nh * hd, dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty(B, nh, T, dtype=torch.float32, device=qkv.device)
+        scale = hd ** -0.5
+        L = _ext.lib()
+        _ext.check(L.nd_attn_fwd(_ext.ptr(q), _ext.ptr(k), _ext.ptr(v), _ext.ptr(o), _ext.ptr(lse),
+                                 B, nh, nkv, T, hd, ld, nh * hd, 0, 0, float(scale), _ext.stream_ptr(qkv.device)),
+                   "nd_attn_fwd")
+        ctx.save_for_backward(qkv_r, o, lse, cos, sin)
+        ctx.dims = (B, T, nh, nkv, hd)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv_r, o, lse, cos, sin = ctx.saved_tensors
+        B, T, nh, nkv, hd = ctx.dims
+        do = do.contiguous()
+        ld = qkv_r.shape[1]
+        L = _ext.lib()
+        dev = do.device
+        delta = torch.empty(B, nh, T, dtype=torch.float32, device=dev)
+        _ext.check(L.nd_attn_bwd_pre(_ext.ptr(o), _ext.ptr(do), _ext.ptr(delta), B, nh, T, hd, nh * hd,
+                                     _ext.stream_ptr(dev)), "nd_attn_bwd_pre")
+        dqkv = torch.empty_like(qkv_r)
+        dq_acc = torch.zeros(B, nh, T, hd, dtype=torch.float32, device=dev)
+        q, k, v = qkv_r, qkv_r[:, nh * hd:], qkv_r[:, (nh + nkv) * hd:]
+        dq, dk, dv = dqkv, dqkv[:, nh * hd:], dqkv[:, (nh + nkv) * hd:]
+        _ext.check(L.nd_attn_bwd(_ext.ptr(q), _ext.ptr(k), _ext.ptr(v), _ext.ptr(do), _ext.ptr(lse), _ext.ptr(delta),
+                                 _ext.ptr(dq), _ext.ptr(dk), _ext.ptr(dv), _ext.ptr(dq_acc),
+                                 B, nh, nkv, T, hd, ld, nh * hd, 0, 0, float(hd ** -0.5), 0,
+                                 _ext.stream_ptr(dev)), "nd_attn_bwd")
+        _rope(dqkv, cos, sin, B, T, nh, nkv, hd, inverse=True)
+        return dqkv, None, None, None, None, None, None, None
+
+
+def attention(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, B: int, T: int, nh: int, nkv: int,
+              hd: int) -> torch.Tensor:
+    """Causal self-attention with RoPE; qkv [B*T, (nh+2nkv)*hd] -> [B*T, nh*hd]."""
+    if _ext.use_hip(qkv):
+        return FlashAttnFn.apply(qkv.contiguous(), cos, sin, B, T, nh, nkv, hd)
+    return ref.attention_block(qkv, cos, sin, B, T, nh, nkv, hd, use_sdpa=True)

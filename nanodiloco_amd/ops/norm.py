@@ -1,0 +1,121 @@
+"""RMSNorm and residual-add + RMSNorm with gradient routing.
+
+Residual stream is kept in fp32 (what HF bf16-autocast effectively does: the embedding output is
+fp32 and every residual add promotes), norm weights are read from the fp32 master, the
+normalised output is emitted in the compute dtype for the next GEMM.
+
+Forward, HIP path: one kernel, one row per wave (``nd_rmsnorm_fwd``) fusing
+``h_new = h + a`` (K8) with ``y = w * h_new * rstd`` (K2) and saving ``rstd``.
+Backward: one kernel producing dx (fp32, already summed with the incoming residual grad) and the
+branch grad in the compute dtype, plus per-block dw partials that are reduced into the flat
+grad buffer.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _ext
+from . import reference as ref
+
+
+def _rows(x):
+    return x.reshape(-1, x.shape[-1])
+
+
+def _hip_fwd(x, a, w, eps, out_dtype):
+    x2 = _rows(x)
+    rows, cols = x2.shape
+    y = torch.empty(rows, cols, dtype=out_dtype, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    h = torch.empty(rows, cols, dtype=torch.float32, device=x.device) if a is not None else None
+    L = _ext.lib()
+    err = L.nd_rmsnorm_fwd(_ext.ptr(x2), _ext.dtcode(x2), _ext.ptr(a), _ext.dtcode(a) if a is not None else 0,
+                           _ext.ptr(w), _ext.ptr(y), _ext.dtcode(y), _ext.ptr(h), _ext.ptr(rstd),
+                           rows, cols, float(eps), _ext.stream_ptr(x.device))
+    _ext.check(err, "nd_rmsnorm_fwd")
+    return y, (h if h is not None else x2), rstd
+
+
+def _hip_bwd(dy, hx, w, rstd, dres, gw, branch_dtype):
+    rows, cols = hx.shape
+    dx = torch.empty(rows, cols, dtype=torch.float32, device=hx.device)
+    da = torch.empty(rows, cols, dtype=branch_dtype, device=hx.device) if branch_dtype is not None else None
+    nblk = min(1024, (rows + 63) // 64)
+    part = torch.empty(nblk, cols, dtype=torch.float32, device=hx.device)
+    L = _ext.lib()
+    dy2 = _rows(dy).contiguous()
+    err = L.nd_rmsnorm_bwd(_ext.ptr(dy2), _ext.dtcode(dy2), _ext.ptr(hx), _ext.ptr(w), _ext.ptr(rstd),
+                           _ext.ptr(dres), _ext.ptr(dx), _ext.dtcode(da) if da is not None else 0,
+                           _ext.ptr(da), rows, cols, _ext.ptr(part), _ext.stream_ptr(hx.device))
+    _ext.check(err, "nd_rmsnorm_bwd")
+    if gw is not None:
+        gw.add_(part.sum(0))
+    return dx, da
+
+
+class RMSNormFn(torch.autograd.Function):
+    """y = rmsnorm(x) * w ; x is the (fp32) residual stream."""
+
+    @staticmethod
+    def forward(ctx, x, w, gw, eps, out_dtype):
+        ctx.eps, ctx.gw, ctx.shape = eps, gw, x.shape
+        if _ext.use_hip(x):
+            y, hx, rstd = _hip_fwd(x, None, w, eps, out_dtype)
+            ctx.save_for_backward(hx, w, rstd)
+            ctx.hip = True
+            return y.view(*x.shape[:-1], x.shape[-1])
+        ctx.hip = False
+        ctx.save_for_backward(x, w)
+        return ref.rmsnorm(x.float(), w, eps).to(out_dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        if ctx.hip:
+            hx, w, rstd = ctx.saved_tensors
+            dx, _ = _hip_bwd(dy, hx, w, rstd, None, ctx.gw, None)
+            return dx.view(ctx.shape), None, None, None, None
+        x, w = ctx.saved_tensors
+        dx, dw = ref.rmsnorm_backward(dy, x, w, ctx.eps)
+        if ctx.gw is not None:
+            ctx.gw.add_(dw)
+        return dx.to(x.dtype), None, None, None, None
+
+
+class AddRMSNormFn(torch.autograd.Function):
+    """h_new = h + a ; y = rmsnorm(h_new) * w.  Returns (y, h_new)."""
+
+    @staticmethod
+    def forward(ctx, h, a, w, gw, eps, out_dtype):
+        ctx.eps, ctx.gw, ctx.shape, ctx.a_dtype = eps, gw, h.shape, a.dtype
+        if _ext.use_hip(h):
+            y, hn, rstd = _hip_fwd(h, _rows(a).contiguous(), w, eps, out_dtype)
+            ctx.save_for_backward(hn, w, rstd)
+            ctx.hip = True
+            return y.view(h.shape), hn.view(h.shape)
+        ctx.hip = False
+        hn = h.float() + a.float()
+        ctx.save_for_backward(hn, w)
+        return ref.rmsnorm(hn, w, eps).to(out_dtype), hn.to(h.dtype)
+
+    @staticmethod
+    def backward(ctx, dy, dhn):
+        if ctx.hip:
+            hn, w, rstd = ctx.saved_tensors
+            dres = _rows(dhn).contiguous() if dhn is not None else None
+            dx, da = _hip_bwd(dy, hn, w, rstd, dres, ctx.gw, ctx.a_dtype)
+            return dx.view(ctx.shape), da.view(ctx.shape), None, None, None, None
+        hn, w = ctx.saved_tensors
+        dx, dw = ref.rmsnorm_backward(dy, hn, w, ctx.eps)
+        if dhn is not None:
+            dx = dx + dhn.float()
+        if ctx.gw is not None:
+            ctx.gw.add_(dw)
+        return dx, dx.to(ctx.a_dtype), None, None, None, None
+
+
+def rmsnorm(x, w, gw, eps, out_dtype=None):
+    return RMSNormFn.apply(x, w, gw, eps, out_dtype or x.dtype)
+
+
+def add_rmsnorm(h, a, w, gw, eps, out_dtype=None):
+    return AddRMSNormFn.apply(h, a, w, gw, eps, out_dtype or a.dtype)

@@ -1,0 +1,124 @@
+"""Bucketed collectives over flat buffers.
+
+Reference: one blocking ``all_reduce(AVG)`` per parameter tensor, 57-201 calls per outer step,
+interleaved with pageable H2D copies (REF/nanodiloco/diloco/diloco.py:46-50).
+
+Here a flat buffer is cut into a few large buckets (default 128 MiB: xGMI rings are per-link
+bound, so a handful of big messages saturate RCCL's channels; tiny per-tensor calls are
+latency-bound).  All buckets are issued back-to-back with ``async_op=True``: RCCL runs them on
+its own communicator stream (the side HIP stream), ordered after the producer kernels already
+queued on the compute stream.  ``wait(i)`` makes the *compute stream* wait for bucket i only --
+the host never blocks -- so a consumer kernel on bucket i overlaps the reduction of bucket i+1.
+
+SUM is used for every backend (gloo has no AVG); the 1/W factor is folded into the consumer
+kernel (outer Nesterov) or into the loss scale (inner DDP).
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+Range = Tuple[int, int]
+
+
+def plan_buckets(start: int, end: int, elem_bytes: int, bucket_bytes: int, align: int = 64) -> List[Range]:
+    per = max(align, (bucket_bytes // elem_bytes) // align * align)
+    out, a = [], start
+    while a < end:
+        b = min(end, a + per)
+        out.append((a, b))
+        a = b
+    return out
+
+
+class CommStats:
+    def __init__(self):
+        self.calls = 0
+        self.bytes = 0
+        self.host_time_s = 0.0
+        self.events: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []
+
+    def reset(self):
+        self.__init__()
+
+
+class PendingAllReduce:
+    def __init__(self, works, ranges, flat):
+        self.works = works
+        self.ranges = ranges
+        self.flat = flat
+        self._done = [False] * len(works)
+
+    def wait(self, i: int):
+        if not self._done[i]:
+            w = self.works[i]
+            if w is not None:
+                w.wait()
+            self._done[i] = True
+
+    def wait_all(self):
+        for i in range(len(self.works)):
+            self.wait(i)
+
+    def __len__(self):
+        return len(self.works)
+
+
+class FlatCommunicator:
+    """Bucketed async all-reduce / broadcast / all-gather on flat buffers for one process group."""
+
+    def __init__(self, group, group_size: int, bucket_mb: float = 128.0, enabled: bool = True):
+        self.group = group
+        self.size = group_size
+        self.bucket_bytes = int(bucket_mb * (1 << 20))
+        self.enabled = enabled and group_size > 1
+        self.stats = CommStats()
+
+    def all_reduce_async(self, flat: torch.Tensor, ranges: Optional[Sequence[Range]] = None) -> PendingAllReduce:
+        if ranges is None:
+            ranges = plan_buckets(0, flat.numel(), flat.element_size(), self.bucket_bytes)
+        works = []
+        t0 = time.perf_counter()
+        for a, b in ranges:
+            if self.enabled:
+                works.append(dist.all_reduce(flat[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+                self.stats.calls += 1
+                self.stats.bytes += (b - a) * flat.element_size()
+            else:
+                works.append(None)
+        self.stats.host_time_s += time.perf_counter() - t0
+        return PendingAllReduce(works, list(ranges), flat)
+
+    def all_reduce(self, flat: torch.Tensor, ranges=None, on_bucket: Optional[Callable[[int, int], None]] = None):
+        p = self.all_reduce_async(flat, ranges)
+        for i, (a, b) in enumerate(p.ranges):
+            p.wait(i)
+            if on_bucket is not None:
+                on_bucket(a, b)
+        return p
+
+    def broadcast(self, flat: torch.Tensor, src_group_rank: int = 0):
+        if not self.enabled:
+            return
+        src = dist.get_global_rank(self.group, src_group_rank) if self.group not in (None, dist.group.WORLD) \
+            else src_group_rank
+        for a, b in plan_buckets(0, flat.numel(), flat.element_size(), self.bucket_bytes):
+            dist.broadcast(flat[a:b], src=src, group=self.group)
+
+    def all_gather_flat(self, flat: torch.Tensor, shard_ranges: Sequence[Range], my_index: int):
+        """Every member contributes ``flat[shard_ranges[my_index]]``; all shards end up everywhere.
+
+        Shards must be equal-sized (the ParamStore pads the flat size to make them so)."""
+        if not self.enabled:
+            return
+        a, b = shard_ranges[my_index]
+        n = b - a
+        if any((y - x) != n for x, y in shard_ranges):
+            raise ValueError("all_gather_flat needs equal shards")
+        lo = shard_ranges[0][0]
+        out = flat[lo:lo + n * len(shard_ranges)]
+        mine = flat[a:b].clone()
+        dist.all_gather_into_tensor(out, mine, group=self.group)

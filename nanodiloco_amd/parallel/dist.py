@@ -1,0 +1,112 @@
+"""Process-group bootstrap and the two-level (inner DDP x outer DiLoCo) topology.
+
+Reference: ``dist.init_process_group("nccl")`` + ``set_device(LOCAL_RANK)``
+(REF/nanodiloco/training_utils/utils.py:41-43), one worker per GPU, one flat group.
+
+Here:
+* backend ``auto`` = ``nccl`` (RCCL over xGMI on MI355X) when GPUs exist, else ``gloo`` (fixes the
+  reference's hard-coded NCCL, SURVEY.md Q8 -- BASELINE config 1 runs on CPU/gloo);
+* world size 1 without torchrun works with no process group at all (collectives become no-ops);
+* ``inner_dp = K`` splits the world into W/K DiLoCo workers of K GPUs each (BASELINE config 3).
+  Inner groups are blocks of K consecutive ranks (xGMI neighbours on one node); outer groups are
+  the ranks with the same index inside their inner group, so an outer all-reduce of shard r only
+  involves the r-th GPU of every worker.
+"""
+from __future__ import annotations
+
+import dataclasses
+import datetime
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclasses.dataclass
+class DistEnv:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = dataclasses.field(default_factory=lambda: torch.device("cpu"))
+    backend: str = "none"
+    inner_dp: int = 1
+    inner_rank: int = 0
+    worker: int = 0           # DiLoCo worker index  (rank // inner_dp)
+    num_workers: int = 1      # world_size // inner_dp
+    inner_group: Optional[object] = None
+    outer_group: Optional[object] = None
+    world_group: Optional[object] = None
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def _env_int(k, d):
+    v = os.environ.get(k)
+    return int(v) if v not in (None, "") else d
+
+
+def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[str] = None,
+                     timeout_s: float = 1800.0) -> DistEnv:
+    rank = _env_int("RANK", 0)
+    world = _env_int("WORLD_SIZE", 1)
+    local_rank = _env_int("LOCAL_RANK", 0)
+    use_cuda = torch.cuda.is_available() and device != "cpu"
+    if backend == "auto":
+        backend = "nccl" if use_cuda else "gloo"
+    if backend == "nccl" and not use_cuda:
+        raise RuntimeError("backend nccl (RCCL) requested but no GPU is visible")
+    if use_cuda:
+        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    if world % inner_dp:
+        raise ValueError(f"world size {world} not divisible by inner_dp {inner_dp}")
+    env = DistEnv(rank=rank, world_size=world, local_rank=local_rank, device=dev, backend="none",
+                  inner_dp=inner_dp, inner_rank=rank % inner_dp, worker=rank // inner_dp,
+                  num_workers=world // inner_dp)
+    if world == 1:
+        return env
+    if not dist.is_initialized():
+        kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = dev  # eager RCCL communicator init
+        dist.init_process_group(**kw)
+    env.backend = backend
+    env.world_group = dist.group.WORLD
+    if inner_dp == 1:
+        env.inner_group = None
+        env.outer_group = dist.group.WORLD
+    else:
+        for w in range(env.num_workers):  # every rank must create every group, in the same order
+            ranks = list(range(w * inner_dp, (w + 1) * inner_dp))
+            g = dist.new_group(ranks)
+            if w == env.worker:
+                env.inner_group = g
+        if env.num_workers > 1:
+            for r in range(inner_dp):
+                ranks = list(range(r, world, inner_dp))
+                g = dist.new_group(ranks)
+                if r == env.inner_rank:
+                    env.outer_group = g
+    return env
+
+
+def destroy_distributed():
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def barrier(env: DistEnv):
+    if env.is_distributed:
+        if env.backend == "nccl":
+            dist.barrier(device_ids=[env.device.index])
+        else:
+            dist.barrier()

@@ -1,0 +1,210 @@
+"""Training driver (capability parity with ``train_model``, REF/nanodiloco/main.py:41-130).
+
+Differences from the reference (each documented in SURVEY.md §3.5 and switchable where cheap):
+* stops after exactly ``total_steps`` inner steps (reference runs one epoch, Q3);
+* gradients are the mean over micro-batches (``legacy_grad_sum=True`` reproduces the reference's
+  sum of micro-batch means, Q1);
+* logs the true mean loss of the inner step on global rank 0 (Q2, Q6), every ``log_every`` steps,
+  so the device is synced only at log points (the reference syncs twice per micro-batch, K10);
+* bf16 compute with fp32 master weights / grads / optimizer state by default on GPU.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+import os
+import time
+from typing import Any, Dict, Optional
+
+import torch
+
+from . import ops
+from .config import LlamaConfig, default_run_config, load_config_from_file, resolve_llama_config
+from .data import build_data
+from .models import LlamaForCausalLM
+from .optim import FlatAdamW, FlatOuterNesterov
+from .parallel.diloco import Diloco
+from .parallel.dist import DistEnv, init_distributed
+from .parallel.inner_ddp import InnerGradSync
+from .utils.logging import make_sink
+from .utils.run_name import create_run_name
+from .utils.seed import set_seed_all
+
+
+@dataclasses.dataclass
+class TrainArgs:
+    # ---- the 13 reference flags (REF/nanodiloco/main.py:42-56), same defaults
+    seed: int = 1337
+    batch_size: int = 256
+    per_device_batch_size: int = 8
+    seq_length: int = 1024
+    warmup_steps: int = 100
+    total_steps: int = 10_000
+    inner_steps: int = 100
+    lr: float = 4e-4
+    outer_lr: float = 0.7
+    project: str = "nano-diloco"
+    dataset_path: str = "/mnt/hf-c4-tiny/datasets/PrimeIntellect/c4-tiny/en/save_to_disk"
+    llama_config_file: Optional[str] = None
+    wandb_config_file: Optional[str] = None
+    # ---- extensions
+    dtype: str = "auto"            # auto | fp32 | bf16
+    data: str = "auto"             # auto | synthetic | memmap | hf
+    ops: str = "auto"              # auto | hip | torch
+    backend: str = "auto"          # auto | nccl | gloo
+    device: str = "auto"           # auto | cpu | cuda
+    inner_dp: int = 1
+    outer_momentum: float = 0.9
+    max_grad_norm: float = 1.0
+    weight_decay: float = 0.01
+    comm_dtype: str = "fp32"
+    bucket_mb: float = 128.0
+    overlap_outer: bool = False
+    offload_snapshot: bool = False
+    legacy_grad_sum: bool = False
+    activation_checkpointing: bool = False
+    checkpoint_dir: Optional[str] = None
+    checkpoint_every: int = 0      # in outer steps (0 = only at the end when checkpoint_dir is set)
+    resume: Optional[str] = None
+    log_every: int = 1
+    log_file: Optional[str] = None
+    wandb: str = "auto"
+    tokenizer: str = "huggyllama/llama-7b"
+    debug_checks: bool = False
+    mask_pad_labels: bool = True
+
+
+def _dtype(name: str, device: torch.device) -> torch.dtype:
+    if name == "auto":
+        return torch.bfloat16 if device.type == "cuda" else torch.float32
+    return {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
+            "bfloat16": torch.bfloat16}[name]
+
+
+def _resolve_data_kind(a: TrainArgs) -> str:
+    if a.data != "auto":
+        return a.data
+    p = a.dataset_path
+    if p and os.path.isdir(p):
+        import glob
+        if glob.glob(os.path.join(p, "*.bin")):
+            return "memmap"
+        return "hf"
+    return "synthetic"
+
+
+class Trainer:
+    def __init__(self, args: TrainArgs, env: Optional[DistEnv] = None):
+        self.args = a = args
+        if a.batch_size % a.per_device_batch_size:
+            raise ValueError("batch_size must be a multiple of per_device_batch_size")  # REF main.py:65
+        if a.total_steps % a.inner_steps:
+            raise ValueError("total_steps must be a multiple of inner_steps")  # REF main.py:69
+        ops.set_backend(a.ops)
+        self.env = env or init_distributed(a.backend, a.inner_dp, device=None if a.device == "auto" else a.device)
+        e = self.env
+        self.llama_config: LlamaConfig = resolve_llama_config(a.llama_config_file)
+        self.run_config = load_config_from_file(a.wandb_config_file) if a.wandb_config_file else default_run_config()
+        set_seed_all(a.seed)
+        self.grad_accum = a.batch_size // a.per_device_batch_size
+        self.outer_steps = a.total_steps // a.inner_steps
+        self.compute_dtype = _dtype(a.dtype, e.device)
+        self.model = LlamaForCausalLM(self.llama_config, e.device, self.compute_dtype,
+                                      activation_checkpointing=a.activation_checkpointing).init_weights(a.seed)
+        inner = FlatAdamW(self.model.store, lr=a.lr, weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm)
+        outer = FlatOuterNesterov(self.model.store, lr=a.outer_lr, momentum=a.outer_momentum)
+        self.diloco = Diloco(self.model, inner, outer, a.warmup_steps, a.total_steps, a.inner_steps, self.outer_steps,
+                             env=e, comm_dtype=_dtype(a.comm_dtype, e.device), bucket_mb=a.bucket_mb,
+                             overlap=a.overlap_outer, offload_snapshot=a.offload_snapshot,
+                             debug_checks=a.debug_checks)
+        self.inner_sync = InnerGradSync(self.model, self.diloco.inner_comm)
+        self.loss_scale = (1.0 if a.legacy_grad_sum else 1.0 / self.grad_accum) / e.inner_dp
+        self.data_kind = _resolve_data_kind(a)
+        self.data = build_data(self.data_kind, vocab_size=self.llama_config.vocab_size, seq_len=a.seq_length,
+                               batch_size=a.per_device_batch_size, seed=a.seed, rank=e.rank, world_size=e.world_size,
+                               device=e.device, dataset_path=a.dataset_path, tokenizer=a.tokenizer,
+                               mask_pad_labels=a.mask_pad_labels)
+        self.start_step = 0
+        if a.resume:
+            from .utils.checkpoint import load_checkpoint
+            st = load_checkpoint(a.resume, self.model, self.diloco, e)
+            self.start_step = int(st["step"])
+            if st.get("data_state") and hasattr(self.data, "load_state_dict"):
+                try:
+                    self.data.load_state_dict(st["data_state"])
+                except Exception:
+                    pass
+        self.run_name = create_run_name("nanodiloco", self.run_config, is_debug=False)
+        self.sink = make_sink(e.rank, a.project, self.run_name, {**self.run_config, **dataclasses.asdict(a)},
+                              jsonl_path=a.log_file, use_wandb=a.wandb)
+
+    # ------------------------------------------------------------------ one inner step
+    def inner_step(self) -> torch.Tensor:
+        """grad_accum micro-batches fwd+bwd, inner-DDP sync, clip+AdamW. Returns mean loss (device)."""
+        loss_sum = None
+        for micro in range(self.grad_accum):
+            batch = next(self.data)
+            if micro == self.grad_accum - 1:
+                self.inner_sync.arm()
+            out = self.model(batch["input_ids"], labels=batch["labels"], loss_scale=self.loss_scale)
+            out.loss.backward()
+            l = out.loss.detach()
+            loss_sum = l if loss_sum is None else loss_sum + l
+        self.inner_sync.finish()
+        self.diloco.inner_step()
+        return loss_sum / self.grad_accum
+
+    def train(self) -> Dict[str, Any]:
+        a, e = self.args, self.env
+        self.model.train()
+        tokens_per_step = a.batch_size * a.seq_length
+        last_t, last_step = time.perf_counter(), self.start_step
+        last_loss = float("nan")
+        for step in range(self.start_step, a.total_steps):
+            loss = self.inner_step()
+            real_step = step + 1
+            did_outer = real_step % a.inner_steps == 0
+            if did_outer:
+                self.diloco.outer_step()
+            if (a.log_every and real_step % a.log_every == 0) or real_step == a.total_steps:
+                lv = float(loss.item())
+                now = time.perf_counter()
+                dt = now - last_t
+                tps = tokens_per_step * (real_step - last_step) * e.world_size / max(dt, 1e-9)
+                last_t, last_step, last_loss = now, real_step, lv
+                metrics = {
+                    "loss": lv,
+                    "step": real_step,
+                    "lr": self.diloco.inner_optimizer.param_groups[0]["lr"],
+                    "Perplexity": math.exp(min(lv, 80.0)),
+                    "effective_step": real_step * e.num_workers,
+                    "total_samples": real_step * a.batch_size * e.world_size,
+                    "tokens_per_s": tps,
+                    "grad_norm": float(self.diloco.inner_optimizer.last_grad_norm.item()),
+                    "outer_step": self.diloco.outer_step_count,
+                }
+                if did_outer:
+                    metrics["bytes_outer"] = self.diloco.bytes_per_outer_step
+                    metrics["sync_s"] = self.diloco.avg_sync_time
+                self.sink.log(metrics)
+            if did_outer and a.checkpoint_dir and a.checkpoint_every and \
+                    (real_step // a.inner_steps) % a.checkpoint_every == 0:
+                self.save(real_step)
+        self.diloco.finalize()
+        if a.checkpoint_dir:
+            self.save(a.total_steps)
+        if e.rank == 0:
+            print("Training completed!", flush=True)
+        self.sink.finish()
+        return {"final_loss": last_loss, "steps": a.total_steps, "outer_steps": self.diloco.outer_step_count}
+
+    def save(self, step: int):
+        from .utils.checkpoint import save_checkpoint
+        ds = self.data.state_dict() if hasattr(self.data, "state_dict") else None
+        save_checkpoint(self.args.checkpoint_dir, self.model, self.diloco, self.env, step, data_state=ds,
+                        extra={"run_name": self.run_name})
+
+
+def train_model(**kwargs) -> Dict[str, Any]:
+    """Programmatic entry with the reference's keyword names (REF/nanodiloco/main.py:41-56)."""
+    return Trainer(TrainArgs(**kwargs)).train()

@@ -1,0 +1,101 @@
+"""Checkpoint / resume (the reference has none -- SURVEY.md §5.4 -- so the format is defined here).
+
+Directory layout (written only at outer-step boundaries, when all replicas are identical):
+
+  <dir>/config.json              HF LlamaConfig JSON (+ "architectures": ["LlamaForCausalLM"])
+  <dir>/model.safetensors        fp32 master weights, HF key names -> ``LlamaForCausalLM.from_pretrained(dir)``
+  <dir>/diloco_state.safetensors outer state shared by all workers: theta_sync, outer momentum
+  <dir>/rank{r}.safetensors      per-rank inner AdamW m/v + data-generator state
+  <dir>/trainer_state.json       step counters, schedule, hyper-params, per-rank scalar state
+
+Only safetensors + JSON: nothing executable is ever deserialised.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Any, Dict, Optional
+
+import torch
+
+from ..parallel.dist import DistEnv, barrier
+
+
+def _save_st(path: str, tensors: Dict[str, torch.Tensor]):
+    from safetensors.torch import save_file
+
+    save_file({k: v.detach().contiguous().cpu() for k, v in tensors.items()}, path + ".tmp")
+    os.replace(path + ".tmp", path)
+
+
+def _load_st(path: str) -> Dict[str, torch.Tensor]:
+    from safetensors.torch import load_file
+
+    return load_file(path)
+
+
+def save_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, step: int, data_state: Optional[Dict[str, Any]] = None,
+                    extra: Optional[Dict[str, Any]] = None):
+    diloco.finalize()
+    os.makedirs(ckpt_dir, exist_ok=True)
+    store = model.store
+    r = env.rank
+    # per-rank state (every rank)
+    per = {"adamw.exp_avg": diloco.inner_optimizer.exp_avg, "adamw.exp_avg_sq": diloco.inner_optimizer.exp_avg_sq}
+    scal: Dict[str, Any] = {"adamw_step": diloco.inner_optimizer.step_count}
+    if data_state:
+        for k, v in data_state.items():
+            if isinstance(v, torch.Tensor):
+                per[f"data.{k}"] = v
+            else:
+                scal[f"data.{k}"] = v
+    _save_st(os.path.join(ckpt_dir, f"rank{r}.safetensors"), per)
+    with open(os.path.join(ckpt_dir, f"rank{r}.json"), "w") as f:
+        json.dump(scal, f)
+    if r == 0:
+        with open(os.path.join(ckpt_dir, "config.json"), "w") as f:
+            json.dump(model.config.to_hf_json(), f, indent=2)
+        _save_st(os.path.join(ckpt_dir, "model.safetensors"), {n: store.master_view(n) for n in store.names})
+        sync = diloco.sync.to(store.device) if diloco.sync.device != store.device else diloco.sync
+        _save_st(os.path.join(ckpt_dir, "diloco_state.safetensors"),
+                 {"theta_sync": sync, "outer_momentum": diloco.outer_optimizer.momentum_buffer})
+        state = {"step": step, "local_step": diloco.local_step, "outer_step_count": diloco.outer_step_count,
+                 "outer_opt_step": diloco.outer_optimizer.step_count, "scheduler": diloco.scheduler.state_dict(),
+                 "world_size": env.world_size, "inner_dp": env.inner_dp, "flat_numel": store.numel,
+                 **(extra or {})}
+        with open(os.path.join(ckpt_dir, "trainer_state.json"), "w") as f:
+            json.dump(state, f, indent=2)
+    barrier(env)
+
+
+def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv) -> Dict[str, Any]:
+    with open(os.path.join(ckpt_dir, "trainer_state.json")) as f:
+        state = json.load(f)
+    store = model.store
+    sd = _load_st(os.path.join(ckpt_dir, "model.safetensors"))
+    model.load_state_dict(sd)
+    ds = _load_st(os.path.join(ckpt_dir, "diloco_state.safetensors"))
+    diloco.sync.copy_(ds["theta_sync"])
+    diloco.outer_optimizer.momentum_buffer.copy_(ds["outer_momentum"])
+    diloco.outer_optimizer.step_count = int(state["outer_opt_step"])
+    diloco.scheduler.load_state_dict(state["scheduler"])
+    diloco.local_step = int(state["local_step"])
+    diloco.outer_step_count = int(state["outer_step_count"])
+    rfile = os.path.join(ckpt_dir, f"rank{env.rank}.safetensors")
+    data_state: Dict[str, Any] = {}
+    if os.path.exists(rfile):
+        per = _load_st(rfile)
+        diloco.inner_optimizer.exp_avg.copy_(per["adamw.exp_avg"])
+        diloco.inner_optimizer.exp_avg_sq.copy_(per["adamw.exp_avg_sq"])
+        with open(os.path.join(ckpt_dir, f"rank{env.rank}.json")) as f:
+            scal = json.load(f)
+        diloco.inner_optimizer.step_count = int(scal["adamw_step"])
+        for k, v in per.items():
+            if k.startswith("data."):
+                data_state[k[5:]] = v
+        for k, v in scal.items():
+            if k.startswith("data."):
+                data_state[k[5:]] = v
+    state["data_state"] = data_state
+    store.sync_shadow()
+    return state
