@@ -1,0 +1,515 @@
+// Causal flash attention forward / backward for gfx950 (MI355X), bf16 in, fp32 accumulate (K6).
+//
+// Inputs are read straight out of the packed q|k|v GEMM output: element (b, t, head, d) of Q is at
+// q[(b*T + t)*ld + head*HD + d] (same for K, V with their own base pointers); O / dO are
+// [B*T, nh*HD] (row stride ldo).  GQA: query head h uses kv head h / (nh/nkv).
+//
+// MFMA: v_mfma_f32_32x32x16_bf16 (32x32 tile, K=16, 64-lane wave).  C/D layout on gfx950:
+// col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5) for accumulator register r (0..15).
+// A/B: lane l holds A[row l&31][k = 8*(l>>5) + j] and B[k = 8*(l>>5) + j][col l&31], j = 0..7.
+// An accumulator X used as the next B operand (registers 8s..8s+7 -> k-step s) carries its rows in
+// the permuted order 16s + 8(j>>2) + 4h + (j&3); the other operand is fetched in that same order
+// with the transposing LDS read ds_read_b64_tr_b16 (4 consecutive rows of one column per lane).
+//
+// Three kernels, all with the same skeleton (4 waves x 32 rows on the lanes, 64-row tiles of the
+// other operand streamed through LDS, register-staged prefetch of tile j+1 issued before the
+// MFMAs of tile j and written to LDS after the next barrier):
+//   fwd   per 128 queries: S^T = K Q^T (query on the lane -> online softmax is a register
+//         reduction + one lane^32 exchange, the O rescale is lane-local), O^T += V^T P^T.
+//   dq    per 128 queries: S^T, dP^T = V dO^T, dS^T = P^T (dP^T - delta), dQ^T += K^T dS^T.
+//   dkdv  per 128 keys (GQA: loops over the group's query heads): S = Q K^T, dP = dO V^T
+//         (key on the lane), dV^T += dO^T P, dK^T += Q^T dS.
+// No atomics and no cross-workgroup reduction anywhere: the backward is bitwise deterministic
+// (DiLoCo replicas stay bit-identical), at the price of recomputing S/dP once more for dQ.
+// LDS tiles are XOR-swizzled at 16-B granularity so the 32 lanes that read 32 different rows at
+// one column spread over the banks; transposed reads compute the same swizzled addresses per lane.
+// Causal: tiles past the diagonal are never loaded; fully masked (wave, tile) pairs are skipped;
+// the longest query / key blocks are dispatched first.
+#include "common.h"
+
+using namespace nd;
+
+typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
+typedef short sv4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bfv8, a), __builtin_bit_cast(bfv8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ sv4 tr_read(const bf16_t* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((sv4 __attribute__((address_space(3)))*)(lds_ptr));
+}
+
+__device__ __forceinline__ bf16x8 cat4(sv4 a, sv4 b) {
+  bf16x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+// Pack accumulator registers 8s..8s+7 into a bf16 MFMA operand fragment.
+__device__ __forceinline__ bf16x8 pack_frag(const f32x16& x, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const uint32_t u = pack2(x[8 * s + j], x[8 * s + j + 1]);
+    r[j] = (short)(u & 0xffff);
+    r[j + 1] = (short)(u >> 16);
+  }
+  return r;
+}
+
+__device__ __forceinline__ bf16x8 load16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ bf16x8 zero8() { return bf16x8{0, 0, 0, 0, 0, 0, 0, 0}; }
+
+// Element offset of (row, col) inside an XOR-swizzled [rows][HD] bf16 LDS tile (16-B chunks).
+template <int HD>
+__device__ __forceinline__ int soff(int row, int col) {
+  constexpr int CPR = HD / 8;                          // 16-B chunks per row
+  constexpr int RPB = (16 / CPR) > 0 ? 16 / CPR : 1;   // rows per 256-B bank row
+  const int ch = (col >> 3) ^ ((row / RPB) & (CPR - 1));
+  return row * HD + ch * 8 + (col & 7);
+}
+
+// A/B fragment with rows on the lanes: row `row`, k-step t, lane half h -> cols 16t + 8h .. +7
+template <int HD>
+__device__ __forceinline__ bf16x8 row_frag(const bf16_t* tile, int row, int t, int h) {
+  return *reinterpret_cast<const bf16x8*>(&tile[soff<HD>(row, 16 * t + 8 * h)]);
+}
+
+// Transposed fragment for the permuted-k operand: rows r0 + 16s + 8(j>>2) + 4h + (j&3), column
+// c0 + (lane & 31).  (g, i) = (lane >> 4, lane & 15).
+template <int HD>
+__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* tile, int rbase, int cbase, int g, int i) {
+  const int row = rbase + 4 * (g >> 1) + (i >> 2);
+  const int col = cbase + 16 * (g & 1) + 4 * (i & 3);
+  return cat4(tr_read(&tile[soff<HD>(row, col)]), tr_read(&tile[soff<HD>(row + 8, col)]));
+}
+
+// Register-staged tile loader: ROWS x HD bf16 tile, 16-B chunks spread over 256 threads.
+template <int ROWS, int HD>
+struct Stage {
+  static constexpr int CPR = HD / 8;
+  static constexpr int N = (ROWS * CPR + 255) / 256;
+  bf16x8 v[N];
+  __device__ __forceinline__ void load(const bf16_t* base, int64_t stride, int row0, int nrows_valid) {
+#pragma unroll
+    for (int it = 0; it < N; ++it) {
+      const int c = threadIdx.x + it * 256;
+      const int row = c / CPR, ch = c % CPR;
+      v[it] = zero8();
+      if (c < ROWS * CPR && row0 + row < nrows_valid) v[it] = load16(base + (int64_t)(row0 + row) * stride + ch * 8);
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* tile) const {
+#pragma unroll
+    for (int it = 0; it < N; ++it) {
+      const int c = threadIdx.x + it * 256;
+      if (c < ROWS * CPR) {
+        const int row = c / CPR, ch = c % CPR;
+        *reinterpret_cast<bf16x8*>(&tile[soff<HD>(row, ch * 8)]) = v[it];
+      }
+    }
+  }
+};
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+// Store a [HD x 32] transposed accumulator (rows = head dim in registers, col = row index on the
+// lane) as 8-B packed bf16 groups into row `r` of a row-major output.
+template <int NO>
+__device__ __forceinline__ void store_T(bf16_t* out_row, const f32x16* acc, float mul, int h) {
+#pragma unroll
+  for (int o = 0; o < NO; ++o)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = o * 32 + 8 * g4 + 4 * h;
+      *reinterpret_cast<uint2*>(out_row + d) =
+          make_uint2(pack2(acc[o][4 * g4 + 0] * mul, acc[o][4 * g4 + 1] * mul),
+                     pack2(acc[o][4 * g4 + 2] * mul, acc[o][4 * g4 + 3] * mul));
+    }
+}
+
+// =============================================================================== forward
+template <int HD>
+__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+                                                          const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
+                                                          float* __restrict__ LSE, int B, int nh, int nkv, int T,
+                                                          int64_t ld, int64_t ldo, float scale) {
+  constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[BN * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[BN * HD];
+
+  const int nqb = (T + 127) / 128, bh_count = B * nh;
+  const int qb = nqb - 1 - (int)(blockIdx.x / bh_count);  // longest causal rows first
+  const int bh = blockIdx.x % bh_count;
+  const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int q0w = qb * 128 + w * 32, qi = q0w + c32;
+  const float c = scale * LOG2E;
+  const bf16_t* Qb = Q + (int64_t)b * T * ld + (int64_t)head * HD;
+  const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
+  const bf16_t* Vb = V + (int64_t)b * T * ld + (int64_t)kvh * HD;
+
+  bf16x8 qf[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) qf[t] = qi < T ? load16(Qb + (int64_t)qi * ld + 16 * t + 8 * h) : zero8();
+  f32x16 oacc[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) oacc[o] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+
+  const int ntiles = (min(T, qb * 128 + 128) + BN - 1) / BN;
+  Stage<BN, HD> sk, sv;
+  sk.load(Kb, ld, 0, T);
+  sv.load(Vb, ld, 0, T);
+  for (int j = 0; j < ntiles; ++j) {
+    const int k0 = j * BN;
+    __syncthreads();
+    sk.store(Ks);
+    sv.store(Vs);
+    __syncthreads();
+    if (j + 1 < ntiles) {  // prefetch the next tile; its latency hides under this tile's MFMAs
+      sk.load(Kb, ld, k0 + BN, T);
+      sv.load(Vb, ld, k0 + BN, T);
+    }
+    if (k0 > q0w + 31) continue;  // whole tile above this wave's diagonal (wave-uniform)
+
+    f32x16 s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = f32x16{};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) s[kt] = mfma32(row_frag<HD>(Ks, kt * 32 + c32, t, h), qf[t], s[kt]);
+    }
+    const bool need_mask = (k0 + BN - 1 > q0w) || (k0 + BN > T);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = s[kt][r] * c;
+        if (need_mask) {
+          const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (key > qi || key >= T) v = -INFINITY;
+        }
+        s[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float alpha = exp2f(m - mnew);
+    m = mnew;
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(s[kt][r] - mnew);
+        s[kt][r] = p;
+        rs += p;
+      }
+    l = l * alpha + rs;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) oacc[o] *= alpha;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx) {
+        const bf16x8 pf = pack_frag(s[kt], sidx);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) oacc[o] = mfma32(tr_frag<HD>(Vs, kt * 32 + 16 * sidx, o * 32, g, i16), pf, oacc[o]);
+      }
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qi < T) {
+    store_T<NO>(O + ((int64_t)b * T + qi) * ldo + (int64_t)head * HD, oacc, inv, h);
+    if (h == 0) LSE[((int64_t)b * nh + head) * T + qi] = m + log2f(lt);
+  }
+}
+
+// =============================================================================== backward
+// delta[b, h, t] = sum_d dO * O   (fp32)
+template <int HD>
+__global__ void __launch_bounds__(256) attn_bwd_pre_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
+                                                           float* __restrict__ delta, int B, int nh, int T, int64_t ldo) {
+  constexpr int CPR = HD / 8;
+  const int64_t rows = (int64_t)B * T * nh;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = gid / CPR;
+  const int ch = (int)(gid % CPR);
+  float acc = 0.f;
+  if (r < rows) {
+    const int64_t bt = r / nh;
+    const int head = (int)(r % nh);
+    float a[8], d[8];
+    Vec8<BF16>::load(O, bt * ldo + (int64_t)head * HD + ch * 8, a);
+    Vec8<BF16>::load(dO, bt * ldo + (int64_t)head * HD + ch * 8, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += a[j] * d[j];
+  }
+#pragma unroll
+  for (int off = CPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (r < rows && ch == 0) {
+    const int64_t bt = r / nh;
+    const int head = (int)(r % nh);
+    const int64_t bb = bt / T, t = bt % T;
+    delta[(bb * nh + head) * T + t] = acc;
+  }
+}
+
+// dQ: per 128 queries of one (b, head), streaming 64-key K/V tiles up to the diagonal.
+template <int HD>
+__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+                                                             const bf16_t* __restrict__ V, const bf16_t* __restrict__ dO,
+                                                             const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                                             bf16_t* __restrict__ dQ, int B, int nh, int nkv, int T,
+                                                             int64_t ld, int64_t ldo, float scale) {
+  constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[BN * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[BN * HD];
+
+  const int nqb = (T + 127) / 128, bh_count = B * nh;
+  const int qb = nqb - 1 - (int)(blockIdx.x / bh_count);
+  const int bh = blockIdx.x % bh_count;
+  const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int q0w = qb * 128 + w * 32, qi = q0w + c32;
+  const float c = scale * LOG2E;
+  const bf16_t* Qb = Q + (int64_t)b * T * ld + (int64_t)head * HD;
+  const bf16_t* dOb = dO + (int64_t)b * T * ldo + (int64_t)head * HD;
+  const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
+  const bf16_t* Vb = V + (int64_t)b * T * ld + (int64_t)kvh * HD;
+
+  bf16x8 qf[NT], dof[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    qf[t] = qi < T ? load16(Qb + (int64_t)qi * ld + 16 * t + 8 * h) : zero8();
+    dof[t] = qi < T ? load16(dOb + (int64_t)qi * ldo + 16 * t + 8 * h) : zero8();
+  }
+  const int64_t rowstat = ((int64_t)b * nh + head) * T;
+  const float lse = qi < T ? LSE[rowstat + qi] : 0.f;
+  const float dlt = qi < T ? DELTA[rowstat + qi] : 0.f;
+  f32x16 dq[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) dq[o] = f32x16{};
+
+  const int ntiles = (min(T, qb * 128 + 128) + BN - 1) / BN;
+  Stage<BN, HD> sk, sv;
+  sk.load(Kb, ld, 0, T);
+  sv.load(Vb, ld, 0, T);
+  for (int j = 0; j < ntiles; ++j) {
+    const int k0 = j * BN;
+    __syncthreads();
+    sk.store(Ks);
+    sv.store(Vs);
+    __syncthreads();
+    if (j + 1 < ntiles) {
+      sk.load(Kb, ld, k0 + BN, T);
+      sv.load(Vb, ld, k0 + BN, T);
+    }
+    if (k0 > q0w + 31) continue;
+    f32x16 s[2], dp[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = f32x16{};
+      dp[kt] = f32x16{};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        s[kt] = mfma32(row_frag<HD>(Ks, kt * 32 + c32, t, h), qf[t], s[kt]);
+        dp[kt] = mfma32(row_frag<HD>(Vs, kt * 32 + c32, t, h), dof[t], dp[kt]);
+      }
+    }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const bool ok = key <= qi && key < T && qi < T;
+        const float p = ok ? exp2f(s[kt][r] * c - lse) : 0.f;
+        dp[kt][r] = p * (dp[kt][r] - dlt);
+      }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx) {
+        const bf16x8 dsf = pack_frag(dp[kt], sidx);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) dq[o] = mfma32(tr_frag<HD>(Ks, kt * 32 + 16 * sidx, o * 32, g, i16), dsf, dq[o]);
+      }
+  }
+  if (qi < T) store_T<NO>(dQ + ((int64_t)b * T + qi) * ld + (int64_t)head * HD, dq, scale, h);
+}
+
+// dK, dV: per 128 keys of one (b, kv head); loops over the GQA group's query heads and 64-query
+// tiles from the diagonal to T.
+template <int HD>
+__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+                                                               const bf16_t* __restrict__ V, const bf16_t* __restrict__ dO,
+                                                               const float* __restrict__ LSE,
+                                                               const float* __restrict__ DELTA, bf16_t* __restrict__ dK,
+                                                               bf16_t* __restrict__ dV, int B, int nh, int nkv, int T,
+                                                               int64_t ld, int64_t ldo, float scale) {
+  constexpr int BQ = 64, NT = HD / 16, NO = HD / 32;
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * HD];
+  __shared__ __attribute__((aligned(16))) float lse_s[BQ];
+  __shared__ __attribute__((aligned(16))) float del_s[BQ];
+
+  const int nkb = (T + 127) / 128, bk_count = B * nkv, rep = nh / nkv;
+  const int kb = (int)(blockIdx.x / bk_count);  // small kb = longest query range: dispatched first
+  const int bk = blockIdx.x % bk_count;
+  const int b = bk / nkv, kvh = bk % nkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int kw0 = kb * 128 + w * 32, key = kw0 + c32;
+  const float c = scale * LOG2E;
+  const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
+  const bf16_t* Vb = V + (int64_t)b * T * ld + (int64_t)kvh * HD;
+  (void)nkb;
+
+  bf16x8 kf[NT], vf[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    kf[t] = key < T ? load16(Kb + (int64_t)key * ld + 16 * t + 8 * h) : zero8();
+    vf[t] = key < T ? load16(Vb + (int64_t)key * ld + 16 * t + 8 * h) : zero8();
+  }
+  f32x16 dk[NO], dv[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) { dk[o] = f32x16{}; dv[o] = f32x16{}; }
+
+  const int qstart = (kb * 128) / BQ * BQ;
+  const int ntq = (T - qstart + BQ - 1) / BQ;
+  const int nit = ntq * rep;
+  Stage<BQ, HD> sq, sd;
+  float lse_n = 0.f, del_n = 0.f;
+  auto prefetch = [&](int it) {
+    const int head = kvh * rep + it / ntq;
+    const int q0 = qstart + (it % ntq) * BQ;
+    sq.load(Q + (int64_t)b * T * ld + (int64_t)head * HD, ld, q0, T);
+    sd.load(dO + (int64_t)b * T * ldo + (int64_t)head * HD, ldo, q0, T);
+    if (threadIdx.x < BQ) {
+      const int qq = q0 + threadIdx.x;
+      const int64_t rs = ((int64_t)b * nh + head) * T;
+      lse_n = qq < T ? LSE[rs + qq] / c : 0.f;
+      del_n = qq < T ? DELTA[rs + qq] : 0.f;
+    }
+  };
+  prefetch(0);
+  for (int it = 0; it < nit; ++it) {
+    const int q0 = qstart + (it % ntq) * BQ;
+    __syncthreads();
+    sq.store(Qs);
+    sd.store(dOs);
+    if (threadIdx.x < BQ) {
+      lse_s[threadIdx.x] = lse_n;
+      del_s[threadIdx.x] = del_n;
+    }
+    __syncthreads();
+    if (it + 1 < nit) prefetch(it + 1);
+#pragma unroll
+    for (int qs = 0; qs < BQ / 32; ++qs) {
+      const int qsub = q0 + qs * 32;
+      if (kw0 > qsub + 31 || kw0 >= T) continue;  // wave-uniform: no query >= any of our keys
+      f32x16 s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        s[r] = -lse_s[qr];
+        dp[r] = -del_s[qr];
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        s = mfma32(row_frag<HD>(Qs, qs * 32 + c32, t, h), kf[t], s);
+        dp = mfma32(row_frag<HD>(dOs, qs * 32 + c32, t, h), vf[t], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qq = qsub + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const bool ok = key <= qq && qq < T && key < T;
+        const float p = ok ? exp2f(s[r] * c) : 0.f;
+        s[r] = p;
+        dp[r] = p * dp[r];
+      }
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx) {
+        const bf16x8 pf = pack_frag(s, sidx);
+        const bf16x8 dsf = pack_frag(dp, sidx);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+          dv[o] = mfma32(tr_frag<HD>(dOs, qs * 32 + 16 * sidx, o * 32, g, i16), pf, dv[o]);
+          dk[o] = mfma32(tr_frag<HD>(Qs, qs * 32 + 16 * sidx, o * 32, g, i16), dsf, dk[o]);
+        }
+      }
+    }
+  }
+  if (key < T) {
+    store_T<NO>(dK + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dk, scale, h);
+    store_T<NO>(dV + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dv, 1.f, h);
+  }
+}
+
+// ------------------------------------------------------------------------------------ launchers
+template <int HD>
+static int fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, int B, int nh, int nkv, int T,
+                      int64_t ld, int64_t ldo, float scale, hipStream_t s) {
+  const int nqb = (T + 127) / 128;
+  hipLaunchKernelGGL(attn_fwd_kernel<HD>, dim3(nqb * B * nh), dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k,
+                     (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale);
+  ND_LAUNCH_CHECK();
+}
+
+ND_API int nd_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int nh, int nkv, int T,
+                       int hd, int64_t ld, int64_t ldo, int64_t /*reserved*/, int64_t /*reserved*/, float scale,
+                       hipStream_t s) {
+  if (nh % nkv || (ld % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
+  switch (hd) {
+    case 32: return fwd_launch<32>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, scale, s);
+    case 64: return fwd_launch<64>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, scale, s);
+    case 128: return fwd_launch<128>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, scale, s);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+ND_API int nd_attn_bwd_pre(const void* o, const void* dout, float* delta, int B, int nh, int T, int64_t hd,
+                           int64_t ldo, hipStream_t s) {
+  const int64_t threads = (int64_t)B * T * nh * (hd / 8);
+  const unsigned grid = (unsigned)((threads + 255) / 256);
+  switch (hd) {
+    case 32: hipLaunchKernelGGL(attn_bwd_pre_kernel<32>, dim3(grid), dim3(256), 0, s, (const bf16_t*)o, (const bf16_t*)dout, delta, B, nh, T, ldo); break;
+    case 64: hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, dim3(grid), dim3(256), 0, s, (const bf16_t*)o, (const bf16_t*)dout, delta, B, nh, T, ldo); break;
+    case 128: hipLaunchKernelGGL(attn_bwd_pre_kernel<128>, dim3(grid), dim3(256), 0, s, (const bf16_t*)o, (const bf16_t*)dout, delta, B, nh, T, ldo); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  ND_LAUNCH_CHECK();
+}
+
+template <int HD>
+static int bwd_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse, const float* delta,
+                      void* dq, void* dk, void* dv, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
+                      hipStream_t s) {
+  const int nb = (T + 127) / 128;
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HD>, dim3(nb * B * nkv), dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k,
+                     (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld,
+                     ldo, scale);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<HD>, dim3(nb * B * nh), dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k,
+                     (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale);
+  ND_LAUNCH_CHECK();
+}
+
+// dq/dk/dv may point into one packed dqkv buffer (row stride ld).  `dqacc` is unused (kept for ABI).
+ND_API int nd_attn_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                       const float* delta, void* dq, void* dk, void* dv, float* /*dqacc*/, int B, int nh, int nkv,
+                       int T, int hd, int64_t ld, int64_t ldo, int64_t /*reserved*/, int64_t /*reserved*/, float scale,
+                       void* /*reserved*/, hipStream_t s) {
+  if (nh % nkv || (ld % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
+  switch (hd) {
+    case 32: return bwd_launch<32>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, scale, s);
+    case 64: return bwd_launch<64>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, scale, s);
+    case 128: return bwd_launch<128>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, scale, s);
+    default: return (int)hipErrorInvalidValue;
+  }
+}

@@ -1,0 +1,101 @@
+"""Build the native libraries in-tree (no JIT cache, no hipify, no torch headers).
+
+  nanodiloco_amd/_lib/libnd_kernels.so   every csrc/*.hip, hipcc --offload-arch=gfx950 -O3
+  nanodiloco_amd/_lib/libnd_runtime.so   csrc/runtime/*.cpp (host C++: token loader), g++ -O3
+
+Usage:  python -m nanodiloco_amd.csrc.build [--force] [--jobs N] [--save-temps]
+Incremental: an object is rebuilt only when its source or a header is newer.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+LIB_DIR = os.path.join(PKG, "_lib")
+OBJ_DIR = os.path.join(PKG, "_lib", "obj")
+ARCH = os.environ.get("ND_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise FileNotFoundError("hipcc not found (ROCm >= 7 required)")
+
+
+def _newer(src_files, target) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in src_files)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build(force: bool = False, jobs: int = 0, save_temps: bool = False, verbose: bool = False) -> dict:
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    hipcc = _hipcc()
+    headers = glob.glob(os.path.join(HERE, "*.h"))
+    sources = sorted(glob.glob(os.path.join(HERE, "*.hip")))
+    flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-I", HERE]
+    if save_temps:
+        flags += ["-save-temps"]
+    todo = []
+    objs = []
+    for s in sources:
+        o = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer([s] + headers, o):
+            todo.append((s, o))
+    jobs = jobs or min(8, os.cpu_count() or 4)
+
+    def comp(so):
+        s, o = so
+        cwd = OBJ_DIR if save_temps else None
+        r = subprocess.run([hipcc] + flags + ["-c", s, "-o", o], capture_output=True, text=True, cwd=cwd)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {os.path.basename(s)}:\n{r.stderr[-6000:]}")
+        return s
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for s in ex.map(comp, todo):
+            if verbose:
+                print(f"[build] compiled {os.path.basename(s)}", flush=True)
+    kern = os.path.join(LIB_DIR, "libnd_kernels.so")
+    if force or todo or _newer(objs, kern):
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", kern + ".tmp"] + objs)
+        os.replace(kern + ".tmp", kern)
+    # host runtime (plain C++)
+    rt_src = sorted(glob.glob(os.path.join(HERE, "runtime", "*.cpp")))
+    rt = os.path.join(LIB_DIR, "libnd_runtime.so")
+    if rt_src and (force or _newer(rt_src, rt)):
+        cxx = shutil.which("g++") or shutil.which("c++")
+        _run([cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", "-o", rt + ".tmp"] + rt_src)
+        os.replace(rt + ".tmp", rt)
+    return {"kernels": kern, "runtime": rt, "compiled": [os.path.basename(s) for s, _ in todo]}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=0)
+    ap.add_argument("--save-temps", action="store_true")
+    a = ap.parse_args(argv)
+    out = build(force=a.force, jobs=a.jobs, save_temps=a.save_temps, verbose=True)
+    print(out)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,93 @@
+// Shared device helpers for the gfx950 (CDNA4 / MI355X) kernels.
+// Wave = 64 lanes everywhere; bf16 is stored as raw uint16 and converted with the native
+// v_cvt_pk_bf16_f32 (via clang's __bf16) -- NaN-preserving, RNE.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ND_API extern "C" __attribute__((visibility("default")))
+
+namespace nd {
+
+constexpr int WAVE = 64;
+enum DType : int { F32 = 0, BF16 = 1 };
+
+typedef uint16_t bf16_t;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));   // MFMA A/B fragment (8 bf16)
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+__device__ __forceinline__ float lo_bf(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// Load / store 8 consecutive elements of either dtype as fp32 (16-B or 32-B vector access).
+template <int DT> struct Vec8;
+template <> struct Vec8<F32> {
+  __device__ __forceinline__ static void load(const void* p, int64_t i, float* v) {
+    const float4* q = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + i);
+    float4 a = q[0], b = q[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ static void store(void* p, int64_t i, const float* v) {
+    float4* q = reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + i);
+    q[0] = make_float4(v[0], v[1], v[2], v[3]);
+    q[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+template <> struct Vec8<BF16> {
+  __device__ __forceinline__ static void load(const void* p, int64_t i, float* v) {
+    uint4 a = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p) + i);
+    v[0] = lo_bf(a.x); v[1] = hi_bf(a.x); v[2] = lo_bf(a.y); v[3] = hi_bf(a.y);
+    v[4] = lo_bf(a.z); v[5] = hi_bf(a.z); v[6] = lo_bf(a.w); v[7] = hi_bf(a.w);
+  }
+  __device__ __forceinline__ static void store(void* p, int64_t i, const float* v) {
+    uint4 a;
+    a.x = pack2(v[0], v[1]); a.y = pack2(v[2], v[3]); a.z = pack2(v[4], v[5]); a.w = pack2(v[6], v[7]);
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p) + i) = a;
+  }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x = NT (multiple of 64). `red` must hold NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (NT == 64) return v;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  return t;
+}
+
+// XCD-aware block remap (bijective for any grid size): consecutive logical tiles land on the
+// same XCD's L2.  blocks b and b+8 share an XCD under round-robin dispatch (speed only).
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int q = nblocks / 8, r = nblocks % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace nd
+
+#define ND_LAUNCH_CHECK() return (int)hipGetLastError()

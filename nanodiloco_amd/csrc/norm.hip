@@ -1,0 +1,200 @@
+// RMSNorm (+ fused residual add) forward / backward for gfx950.
+//
+// Memory-bound: one 64-lane wave owns one row; each lane holds NCH chunks of 8 contiguous
+// elements (16-B bf16 / 32-B fp32 vector accesses, Guideline 13), so a row is read exactly once
+// from HBM and reduced with a wave butterfly (no LDS, no block barrier in the forward).
+// Forward fuses h_new = h + a (residual, fp32) with y = w * h_new * rstd (compute dtype) and
+// saves rstd.  Backward recomputes xhat from (h_new, rstd), adds the incoming residual gradient,
+// emits dx (fp32) and optionally the branch gradient in the compute dtype, and accumulates
+// dw = sum_rows dy * xhat per lane in registers across the rows a wave visits; the 4 waves of a
+// block combine through LDS and write one partial row per block (host reduces <=1024 partials).
+#include "common.h"
+
+using namespace nd;
+
+template <int NCH, int XDT, int ADT, int YDT>
+__global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const void* __restrict__ x, const void* __restrict__ a,
+                                                          const float* __restrict__ w, void* __restrict__ y,
+                                                          float* __restrict__ h_out, float* __restrict__ rstd_out,
+                                                          int64_t rows, int cols, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t r = wave; r < rows; r += nwaves) {
+    float v[NCH][8];
+    float ss = 0.f;
+    const int64_t base = r * cols;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col < cols) {
+        Vec8<XDT>::load(x, base + col, v[c]);
+        if (ADT >= 0) {
+          float t[8];
+          Vec8<(ADT >= 0 ? ADT : 0)>::load(a, base + col, t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[c][j] += t[j];
+          Vec8<F32>::store(h_out, base + col, v[c]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+      }
+    }
+    ss = wave_sum(ss);
+    const float rs = rsqrtf(ss / (float)cols + eps);
+    if (lane == 0) rstd_out[r] = rs;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col < cols) {
+        float wv[8], o[8];
+        Vec8<F32>::load(w, col, wv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = wv[j] * (v[c][j] * rs);
+        Vec8<YDT>::store(y, base + col, o);
+      }
+    }
+  }
+}
+
+template <int NCH, int DYDT, int DADT>
+__global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const void* __restrict__ dy, const float* __restrict__ h,
+                                                          const float* __restrict__ w, const float* __restrict__ rstd,
+                                                          const float* __restrict__ dres, float* __restrict__ dx,
+                                                          void* __restrict__ da, float* __restrict__ part,
+                                                          int64_t rows, int cols) {
+  extern __shared__ __attribute__((aligned(16))) float sdw[];
+  const int lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < cols; i += 256) sdw[i] = 0.f;
+  __syncthreads();
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  float dwacc[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dwacc[c][j] = 0.f;
+  float wv[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < cols) Vec8<F32>::load(w, col, wv[c]);
+  }
+  for (int64_t r = wave; r < rows; r += nwaves) {
+    const int64_t base = r * cols;
+    const float rs = rstd[r];
+    float g[NCH][8], xh[NCH][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col < cols) {
+        float d[8];
+        Vec8<DYDT>::load(dy, base + col, d);
+        Vec8<F32>::load(h, base + col, xh[c]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[c][j] *= rs;
+          g[c][j] = d[j] * wv[c][j];
+          dot += g[c][j] * xh[c][j];
+          dwacc[c][j] += d[j] * xh[c][j];
+        }
+      }
+    }
+    dot = wave_sum(dot) / (float)cols;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col < cols) {
+        float o[8];
+        if (dres) Vec8<F32>::load(dres, base + col, o);
+        else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += rs * (g[c][j] - xh[c][j] * dot);
+        Vec8<F32>::store(dx, base + col, o);
+        if (DADT >= 0) Vec8<(DADT >= 0 ? DADT : 0)>::store(da, base + col, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < cols)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) atomicAdd(&sdw[col + j], dwacc[c][j]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < cols; i += 256) part[(int64_t)blockIdx.x * cols + i] = sdw[i];
+}
+
+// ------------------------------------------------------------------------------------ launchers
+template <int NCH>
+static int fwd_dispatch(const void* x, int xdt, const void* a, int adt, const float* w, void* y, int ydt, float* h,
+                        float* rstd, int64_t rows, int cols, float eps, hipStream_t s) {
+  int64_t blocks = (rows + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  dim3 g((unsigned)blocks), b(256);
+#define ND_RF(X, A, Y) hipLaunchKernelGGL((rmsnorm_fwd_kernel<NCH, X, A, Y>), g, b, 0, s, x, a, w, y, h, rstd, rows, cols, eps)
+  if (a == nullptr) {
+    if (xdt == F32 && ydt == BF16) ND_RF(F32, -1, BF16);
+    else if (xdt == F32 && ydt == F32) ND_RF(F32, -1, F32);
+    else if (xdt == BF16 && ydt == BF16) ND_RF(BF16, -1, BF16);
+    else return (int)hipErrorInvalidValue;
+  } else {
+    if (xdt == F32 && adt == BF16 && ydt == BF16) ND_RF(F32, BF16, BF16);
+    else if (xdt == F32 && adt == F32 && ydt == F32) ND_RF(F32, F32, F32);
+    else if (xdt == F32 && adt == F32 && ydt == BF16) ND_RF(F32, F32, BF16);
+    else return (int)hipErrorInvalidValue;
+  }
+#undef ND_RF
+  ND_LAUNCH_CHECK();
+}
+
+ND_API int nd_rmsnorm_fwd(const void* x, int xdt, const void* a, int adt, const float* w, void* y, int ydt, float* h,
+                          float* rstd, int64_t rows, int cols, float eps, hipStream_t s) {
+  if (cols % 8 || cols > 8 * 512) return (int)hipErrorInvalidValue;
+  const int nch = (cols + 511) / 512;
+  switch (nch) {
+    case 1: return fwd_dispatch<1>(x, xdt, a, adt, w, y, ydt, h, rstd, rows, cols, eps, s);
+    case 2: return fwd_dispatch<2>(x, xdt, a, adt, w, y, ydt, h, rstd, rows, cols, eps, s);
+    case 3: case 4: return fwd_dispatch<4>(x, xdt, a, adt, w, y, ydt, h, rstd, rows, cols, eps, s);
+    default: return fwd_dispatch<8>(x, xdt, a, adt, w, y, ydt, h, rstd, rows, cols, eps, s);
+  }
+}
+
+template <int NCH>
+static int bwd_dispatch(const void* dy, int dydt, const float* h, const float* w, const float* rstd, const float* dres,
+                        float* dx, int dadt, void* da, int64_t rows, int cols, float* part, hipStream_t s) {
+  int64_t blocks = (rows + 63) / 64;
+  if (blocks > 1024) blocks = 1024;
+  dim3 g((unsigned)blocks), b(256);
+  size_t lds = (size_t)cols * sizeof(float);
+#define ND_RB(D, A) hipLaunchKernelGGL((rmsnorm_bwd_kernel<NCH, D, A>), g, b, lds, s, dy, h, w, rstd, dres, dx, da, part, rows, cols)
+  if (da == nullptr) {
+    if (dydt == BF16) ND_RB(BF16, -1); else ND_RB(F32, -1);
+  } else {
+    if (dydt == BF16 && dadt == BF16) ND_RB(BF16, BF16);
+    else if (dydt == F32 && dadt == F32) ND_RB(F32, F32);
+    else if (dydt == BF16 && dadt == F32) ND_RB(BF16, F32);
+    else ND_RB(F32, BF16);
+  }
+#undef ND_RB
+  ND_LAUNCH_CHECK();
+}
+
+// part must hold min(1024, ceil(rows/64)) * cols floats (the Python side allocates exactly that).
+ND_API int nd_rmsnorm_bwd(const void* dy, int dydt, const float* h, const float* w, const float* rstd,
+                          const float* dres, float* dx, int dadt, void* da, int64_t rows, int cols, float* part,
+                          hipStream_t s) {
+  if (cols % 8 || cols > 8 * 512) return (int)hipErrorInvalidValue;
+  const int nch = (cols + 511) / 512;
+  switch (nch) {
+    case 1: return bwd_dispatch<1>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
+    case 2: return bwd_dispatch<2>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
+    case 3: case 4: return bwd_dispatch<4>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
+    default: return bwd_dispatch<8>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
+  }
+}

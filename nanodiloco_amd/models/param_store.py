@@ -52,7 +52,10 @@ class ParamStore:
             self.shapes[name] = shape
             self.offsets[name] = off
             off += _numel(shape)
-        self.numel = (off + align - 1) // align * align
+        # pad so the flat vector splits into 1..8 equal, 64-aligned shards (lcm(1..8) = 840):
+        # the two-level outer step shards it over the GPUs of one DiLoCo worker.
+        q = align * 840
+        self.numel = (off + q - 1) // q * q
         self.num_params = sum(_numel(s) for s in self.shapes.values())
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)

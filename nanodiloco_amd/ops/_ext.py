@@ -22,7 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(os.path.dirname(_HERE), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libnd_kernels.so")
 
-_lib: Optional[ctypes.CDLL] = None
+_lib = None
 _lock = threading.Lock()
 _backend = os.environ.get("NANODILOCO_OPS", "auto")  # auto | hip | torch
 
@@ -51,8 +51,9 @@ def lib() -> ctypes.CDLL:
                     raise ExtensionMissing(
                         f"HIP kernel library not found at {LIB_PATH}. Build it with "
                         f"`python -m nanodiloco_amd.csrc.build` (or __graft_entry__.build()).")
-                _lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-                _declare(_lib)
+                raw = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+                _declare(raw)
+                _lib = _StrictLib(raw)
     return _lib
 
 
@@ -119,7 +120,7 @@ def _declare(L: ctypes.CDLL):
         "nd_embedding_bwd": [P, P, P, L64, I, I, P],
         # optimizer / outer step (flat buffers)
         "nd_sumsq_partial": [P, L64, P, I, P],
-        "nd_adamw_step": [P, P, P, P, P, I, L64, P, I, F, F, F, F, F, F, F, F, P],
+        "nd_adamw_step": [P, P, P, P, P, I, L64, P, I, F, F, F, F, F, F, F, F, P, P],
         "nd_pseudograd": [P, P, P, I, L64, P],
         "nd_outer_nesterov": [P, P, P, I, P, P, I, L64, F, F, F, I, P, P, P],
         "nd_axpby": [P, P, L64, F, F, P],
@@ -130,6 +131,29 @@ def _declare(L: ctypes.CDLL):
             continue
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int
+
+
+class _StrictLib:
+    """ctypes silently accepts surplus positional arguments (and then passes garbage through the
+    C ABI); every launcher call is checked against its declared arity instead."""
+
+    def __init__(self, raw):
+        self._raw = raw
+        self._fns = {}
+
+    def __getattr__(self, name):
+        f = self._fns.get(name)
+        if f is None:
+            fn = getattr(self._raw, name)
+            n = len(fn.argtypes) if fn.argtypes is not None else None
+
+            def f(*args, _fn=fn, _n=n, _name=name):
+                if _n is not None and len(args) != _n:
+                    raise TypeError(f"{_name}: expected {_n} arguments, got {len(args)}")
+                return _fn(*args)
+
+            self._fns[name] = f
+        return f
 
 
 def check(err: int, what: str):

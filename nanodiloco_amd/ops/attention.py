@@ -8,8 +8,9 @@ write ``O`` as ``[B*T, nh*hd]`` -- exactly the o_proj GEMM input.
 HIP path
   fwd: ``nd_rope_inplace`` on a copy of q|k (half-split rotation, fp32 tables)
        ``nd_attn_fwd``  -- MFMA flash attention, online softmax, saves LSE (fp32, log2 domain)
-  bwd: ``nd_attn_bwd_pre`` (delta = rowsum(dO * O)), ``nd_attn_bwd`` (dQ, dK, dV; recomputes P from
-       LSE), ``nd_rope_inplace(inverse)`` on dq|dk.
+  bwd: ``nd_attn_bwd_pre`` (delta = rowsum(dO * O)), ``nd_attn_bwd`` = a key-parallel dK/dV kernel
+       and a query-parallel dQ kernel (both recompute P from LSE; no atomics -> deterministic),
+       then ``nd_rope_inplace(inverse)`` on dq|dk.
 GQA (nkv < nh) is handled by head-index mapping inside the kernels (no K/V repetition).
 """
 from __future__ import annotations
@@ -73,11 +74,10 @@ class FlashAttnFn(torch.autograd.Function):
         _ext.check(L.nd_attn_bwd_pre(_ext.ptr(o), _ext.ptr(do), _ext.ptr(delta), B, nh, T, hd, nh * hd,
                                      _ext.stream_ptr(dev)), "nd_attn_bwd_pre")
         dqkv = torch.empty_like(qkv_r)
-        dq_acc = torch.zeros(B, nh, T, hd, dtype=torch.float32, device=dev)
         q, k, v = qkv_r, qkv_r[:, nh * hd:], qkv_r[:, (nh + nkv) * hd:]
         dq, dk, dv = dqkv, dqkv[:, nh * hd:], dqkv[:, (nh + nkv) * hd:]
         _ext.check(L.nd_attn_bwd(_ext.ptr(q), _ext.ptr(k), _ext.ptr(v), _ext.ptr(do), _ext.ptr(lse), _ext.ptr(delta),
-                                 _ext.ptr(dq), _ext.ptr(dk), _ext.ptr(dv), _ext.ptr(dq_acc),
+                                 _ext.ptr(dq), _ext.ptr(dk), _ext.ptr(dv), 0,
                                  B, nh, nkv, T, hd, ld, nh * hd, 0, 0, float(hd ** -0.5), 0,
                                  _ext.stream_ptr(dev)), "nd_attn_bwd")
         _rope(dqkv, cos, sin, B, T, nh, nkv, hd, inverse=True)

@@ -204,11 +204,13 @@ class Diloco:
     # ------------------------------------------------------------------ debug
     @torch.no_grad()
     def check_replicas(self, tol: float = 0.0):
-        """Assert all replicas hold identical weights: checksum all-reduce MAX-MIN."""
+        """Assert all replicas hold identical outer weights theta_sync: checksum
+        all-reduce MAX-MIN.  (In the overlapped mode the local weights legitimately differ by each
+        worker's in-flight inner progress, so the synced snapshot is what must agree.)"""
         if not self.env.is_distributed:
             return
         import torch.distributed as dist
-        m = self.store.master
+        m = self.sync.to(self.store.device)
         v = torch.stack([m.double().sum(), (m.double() * torch.arange(1, m.numel() + 1, device=m.device,
                                                                       dtype=torch.float64).remainder(7)).sum()])
         mx, mn = v.clone(), v.clone()

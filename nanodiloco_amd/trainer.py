@@ -65,6 +65,7 @@ class TrainArgs:
     activation_checkpointing: bool = False
     checkpoint_dir: Optional[str] = None
     checkpoint_every: int = 0      # in outer steps (0 = only at the end when checkpoint_dir is set)
+    stop_at_step: int = 0          # stop early (simulated preemption) after this inner step; 0 = run to total
     resume: Optional[str] = None
     log_every: int = 1
     log_file: Optional[str] = None
@@ -190,8 +191,10 @@ class Trainer:
             if did_outer and a.checkpoint_dir and a.checkpoint_every and \
                     (real_step // a.inner_steps) % a.checkpoint_every == 0:
                 self.save(real_step)
+            if a.stop_at_step and real_step >= a.stop_at_step:
+                break
         self.diloco.finalize()
-        if a.checkpoint_dir:
+        if a.checkpoint_dir and not a.stop_at_step:
             self.save(a.total_steps)
         if e.rank == 0:
             print("Training completed!", flush=True)

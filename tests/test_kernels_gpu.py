@@ -1,0 +1,227 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (T3)."""
+import math
+
+import pytest
+import torch
+
+from nanodiloco_amd import ops
+from nanodiloco_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _hip(hip_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ops.set_backend("hip")
+    torch.manual_seed(0)
+    yield
+    ops.set_backend("auto")
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+# ----------------------------------------------------------------------------------- rmsnorm
+@pytest.mark.parametrize("cols", [128, 1024, 2048])
+@pytest.mark.parametrize("residual", [False, True])
+def test_rmsnorm_fwd_bwd(cols, residual):
+    rows, eps = 1000, 1e-5
+    h = torch.randn(rows, cols, device=DEV)
+    a = torch.randn(rows, cols, device=DEV).bfloat16()
+    w = (1 + 0.1 * torch.randn(cols, device=DEV))
+    gw = torch.zeros(cols, device=DEV)
+    hr = h.clone().requires_grad_(True)
+    ar = a.clone().float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    hh = hr + ar if residual else hr
+    yr = wr * (hh * torch.rsqrt(hh.pow(2).mean(-1, keepdim=True) + eps))
+    hx = h.clone().requires_grad_(True)
+    ax = a.clone().requires_grad_(True)
+    if residual:
+        y, hn = ops.add_rmsnorm(hx, ax, w, gw, eps, torch.bfloat16)
+        assert rel(hn, (h + a.float())) < 1e-6
+    else:
+        y = ops.rmsnorm(hx, w, gw, eps, torch.bfloat16)
+    assert y.dtype == torch.bfloat16
+    assert rel(y, yr) < 5e-3
+    dy = torch.randn(rows, cols, device=DEV)
+    (yr * dy).sum().backward()
+    (y.float() * dy.bfloat16().float()).sum().backward()
+    assert rel(hx.grad, hr.grad) < 1e-2
+    assert rel(gw, wr.grad) < 1e-2
+    if residual:
+        assert rel(ax.grad, ar.grad) < 1e-2
+
+
+# ----------------------------------------------------------------------------------- rope
+@pytest.mark.parametrize("hd,nh,nkv", [(64, 4, 4), (128, 4, 2), (32, 4, 1)])
+def test_rope_inplace_matches_reference(hd, nh, nkv, hip_lib):
+    from nanodiloco_amd.ops import _ext
+    from nanodiloco_amd.ops.attention import _rope, rope_cache
+
+    B, T = 2, 96
+    ld = (nh + 2 * nkv) * hd
+    qkv = torch.randn(B * T, ld, device=DEV).bfloat16()
+    cos, sin = rope_cache(T, hd, 10000.0, None, DEV)
+    out = qkv.clone()
+    _rope(out, cos, sin, B, T, nh, nkv, hd, inverse=False)
+    q, k, v = ref.split_qkv(qkv.float(), B, T, nh, nkv, hd)
+    qr = ref.apply_rope(q, cos, sin)
+    kr = ref.apply_rope(k, cos, sin)
+    q2, k2, v2 = ref.split_qkv(out.float(), B, T, nh, nkv, hd)
+    assert rel(q2, qr) < 5e-3 and rel(k2, kr) < 5e-3
+    assert torch.equal(v2, v)
+    back = out.clone()
+    _rope(back, cos, sin, B, T, nh, nkv, hd, inverse=True)
+    assert rel(back, qkv) < 1e-2
+
+
+# ----------------------------------------------------------------------------------- swiglu
+@pytest.mark.parametrize("F", [512, 2688])
+def test_swiglu(F):
+    n = 777
+    gu = torch.randn(n, 2 * F, device=DEV).bfloat16().requires_grad_(True)
+    gr = gu.detach().float().requires_grad_(True)
+    y = ops.swiglu(gu)
+    yr = ref.swiglu(gr)
+    assert rel(y, yr) < 5e-3
+    dy = torch.randn(n, F, device=DEV).bfloat16()
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert rel(gu.grad, gr.grad) < 1e-2
+
+
+# ----------------------------------------------------------------------------------- embedding
+def test_embedding():
+    V, d, n = 1000, 256, 4096
+    W = torch.randn(V, d, device=DEV)
+    gW = torch.zeros(V, d, device=DEV)
+    ids = torch.randint(0, V, (4, n // 4), device=DEV)
+    out = ops.embedding(ids, W, gW)
+    assert torch.equal(out, W[ids.reshape(-1)])
+    dy = torch.randn(n, d, device=DEV)
+    out.backward(dy)
+    ref_g = torch.zeros(V, d, device=DEV).index_add_(0, ids.reshape(-1), dy)
+    assert rel(gW, ref_g) < 1e-6
+
+
+# ----------------------------------------------------------------------------------- fused lm_head + CE
+@pytest.mark.parametrize("V", [32000, 1000, 50257])
+def test_lm_head_ce(V):
+    n, d = 640, 256
+    y = (0.5 * torch.randn(n, d, device=DEV)).bfloat16().requires_grad_(True)
+    W = (0.05 * torch.randn(V, d, device=DEV)).bfloat16()
+    gW = torch.zeros(V, d, device=DEV)
+    tgt = torch.randint(0, V, (n,), device=DEV)
+    tgt[::7] = -100
+    scale = 0.25
+    loss = ops.lm_head_ce(y, W, gW, tgt, loss_scale=scale, chunk_rows=256)
+    loss.backward()
+    yr = y.detach().float().requires_grad_(True)
+    Wr = W.float().requires_grad_(True)
+    lr_ = torch.nn.functional.cross_entropy(yr @ Wr.t(), tgt, ignore_index=-100)
+    (lr_ * scale).backward()
+    assert abs(loss.item() - lr_.item()) < 2e-3 * max(1.0, abs(lr_.item()))
+    assert rel(y.grad, yr.grad) < 2e-2
+    assert rel(gW, Wr.grad) < 2e-2
+
+
+# ----------------------------------------------------------------------------------- attention
+def _attn_ref(qkv, cos, sin, B, T, nh, nkv, hd):
+    q, k, v = ref.split_qkv(qkv.float(), B, T, nh, nkv, hd)
+    q = ref.apply_rope(q, cos, sin)
+    k = ref.apply_rope(k, cos, sin)
+    o = ref.causal_attention(q, k, v)
+    return o.transpose(1, 2).reshape(B * T, nh * hd)
+
+
+@pytest.mark.parametrize("B,T,nh,nkv,hd", [
+    (2, 64, 2, 2, 64), (2, 200, 4, 4, 64), (1, 1024, 2, 2, 64), (2, 256, 4, 1, 64),
+    (2, 130, 4, 4, 32), (1, 300, 2, 1, 128), (1, 2048, 1, 1, 64),
+])
+def test_flash_attention_fwd_bwd(B, T, nh, nkv, hd):
+    from nanodiloco_amd.ops.attention import rope_cache
+
+    ld = (nh + 2 * nkv) * hd
+    qkv = torch.randn(B * T, ld, device=DEV).bfloat16()
+    cos, sin = rope_cache(T, hd, 10000.0, None, DEV)
+    x = qkv.clone().requires_grad_(True)
+    o = ops.attention(x, cos, sin, B, T, nh, nkv, hd)
+    xr = qkv.float().requires_grad_(True)
+    orf = _attn_ref(xr, cos, sin, B, T, nh, nkv, hd)
+    assert o.shape == (B * T, nh * hd)
+    assert rel(o, orf) < 1e-2, rel(o, orf)
+    do = torch.randn_like(orf)
+    o.backward(do.bfloat16())
+    orf.backward(do.bfloat16().float())
+    g, gr = x.grad.float(), xr.grad
+    nq, nk = nh * hd, nkv * hd
+    assert rel(g[:, :nq], gr[:, :nq]) < 3e-2, ("dq", rel(g[:, :nq], gr[:, :nq]))
+    assert rel(g[:, nq:nq + nk], gr[:, nq:nq + nk]) < 3e-2, ("dk", rel(g[:, nq:nq + nk], gr[:, nq:nq + nk]))
+    assert rel(g[:, nq + nk:], gr[:, nq + nk:]) < 3e-2, ("dv", rel(g[:, nq + nk:], gr[:, nq + nk:]))
+
+
+def test_flash_attention_softmax_spike():
+    """Force a large max jump mid-sequence (online-softmax rescale path, rule 26)."""
+    from nanodiloco_amd.ops.attention import rope_cache
+
+    B, T, nh, nkv, hd = 1, 512, 1, 1, 64
+    ld = (nh + 2 * nkv) * hd
+    qkv = torch.randn(B * T, ld, device=DEV)
+    qkv[300, nh * hd:(nh + nkv) * hd] *= 30.0  # one key row with a huge score for many queries
+    qkv = qkv.bfloat16()
+    cos, sin = rope_cache(T, hd, 10000.0, None, DEV)
+    o = ops.attention(qkv, cos, sin, B, T, nh, nkv, hd)
+    orf = _attn_ref(qkv, cos, sin, B, T, nh, nkv, hd)
+    assert rel(o, orf) < 1e-2
+
+
+# ----------------------------------------------------------------------------------- optimizers
+def test_adamw_matches_torch():
+    n = 100_003 + 64 - (100_003 % 64)
+    p0 = torch.randn(n, device=DEV)
+    grads = [torch.randn(n, device=DEV) * 3 for _ in range(3)]
+    # torch reference
+    p = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.AdamW([p], lr=1e-3, weight_decay=0.01)
+    for g in grads:
+        p.grad = g.clone()
+        torch.nn.utils.clip_grad_norm_([p], 1.0)
+        opt.step()
+    # ours
+    master = p0.clone()
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    sh = torch.zeros(n, device=DEV, dtype=torch.bfloat16)
+    norm = torch.zeros(1, device=DEV)
+    for i, g in enumerate(grads):
+        ops.adamw_step(master, g.clone(), m, v, sh, i + 1, 1e-3, (0.9, 0.999), 1e-8, 0.01, 1.0, norm_out=norm)
+    assert (master - p.detach()).abs().max().item() < 1e-5
+    assert abs(norm.item() - grads[-1].norm().item()) / grads[-1].norm().item() < 1e-4
+    assert torch.equal(sh, master.bfloat16())
+
+
+@pytest.mark.parametrize("comm", [torch.float32, torch.bfloat16])
+def test_outer_nesterov_matches_torch_sgd(comm):
+    n = 4096
+    sync = torch.randn(n, device=DEV)
+    local = sync - 0.01 * torch.randn(n, device=DEV)
+    # torch reference: param = sync, grad = avg delta, SGD nesterov
+    p = torch.nn.Parameter(sync.clone())
+    opt = torch.optim.SGD([p], lr=0.7, momentum=0.9, nesterov=True)
+    delta = torch.empty(n, device=DEV, dtype=comm)
+    ops.pseudograd(sync, local, delta)
+    p.grad = delta.float().clone()
+    opt.step()
+    master = local.clone()
+    s2 = sync.clone()
+    mom = torch.zeros(n, device=DEV)
+    ops.outer_nesterov(master, s2, delta, mom, None, 1.0, 0.7, 0.9, True)
+    assert (master - p.detach()).abs().max().item() < 1e-6
+    assert torch.equal(master, s2)

@@ -1,0 +1,80 @@
+"""T2: our Llama (PyTorch path) vs HF LlamaForCausalLM with the same weights (fp32)."""
+import pytest
+import torch
+
+from nanodiloco_amd.config import LlamaConfig
+from nanodiloco_amd.models import LlamaForCausalLM, ParamStore
+
+transformers = pytest.importorskip("transformers")
+
+
+@pytest.mark.parametrize("cfgd", [
+    dict(hidden_size=64, intermediate_size=128, num_attention_heads=4, num_hidden_layers=2, vocab_size=97),
+    dict(hidden_size=64, intermediate_size=96, num_attention_heads=4, num_key_value_heads=2, num_hidden_layers=2,
+         vocab_size=101, rms_norm_eps=1e-5),
+    dict(hidden_size=32, intermediate_size=64, num_attention_heads=2, num_hidden_layers=1, vocab_size=64,
+         tie_word_embeddings=True),
+])
+def test_logits_loss_grads_match_hf(cfgd):
+    torch.manual_seed(0)
+    c = LlamaConfig.from_dict(cfgd)
+    m = LlamaForCausalLM(c).init_weights(1)
+    hf = transformers.LlamaForCausalLM(transformers.LlamaConfig(**cfgd, attn_implementation="eager")).float()
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    hf.load_state_dict(sd, strict=False)
+    if c.tie_word_embeddings:
+        hf.tie_weights()
+    ids = torch.randint(0, c.vocab_size, (3, 24))
+    labels = ids.clone()
+    labels[0, :5] = -100
+    out = m(ids, labels=labels)
+    out.loss.backward()
+    ho = hf(input_ids=ids, labels=labels)
+    ho.loss.backward()
+    assert abs(out.loss.item() - ho.loss.item()) < 1e-5
+    for n, p in hf.named_parameters():
+        assert torch.allclose(p.grad, m.store.grad_view(n), atol=2e-6, rtol=1e-4), n
+    logits = m(ids).logits
+    assert torch.allclose(logits, ho.logits, atol=1e-5)
+
+
+def test_loss_scale_scales_grads_only():
+    c = LlamaConfig.from_dict(dict(hidden_size=32, intermediate_size=64, num_attention_heads=2,
+                                   num_hidden_layers=1, vocab_size=50))
+    m = LlamaForCausalLM(c).init_weights(0)
+    ids = torch.randint(0, 50, (2, 16))
+    l1 = m(ids, labels=ids).loss
+    l1.backward()
+    g1 = m.store.grad.clone()
+    m.store.zero_grad()
+    l2 = m(ids, labels=ids, loss_scale=0.25).loss
+    l2.backward()
+    assert torch.allclose(l1, l2)
+    assert torch.allclose(m.store.grad, 0.25 * g1, atol=1e-7)
+
+
+def test_param_store_layout():
+    c = LlamaConfig.from_dict(dict(hidden_size=64, intermediate_size=128, num_attention_heads=4,
+                                   num_key_value_heads=2, num_hidden_layers=2, vocab_size=100))
+    m = LlamaForCausalLM(c)
+    st = m.store
+    assert st.numel % (64 * 840) == 0
+    for n in st.names:
+        assert st.offsets[n] % 64 == 0 or "k_proj" in n or "v_proj" in n or "up_proj" in n
+    qkv = st.fused_view("master", ["model.layers.0.self_attn.q_proj.weight", "model.layers.0.self_attn.k_proj.weight",
+                                   "model.layers.0.self_attn.v_proj.weight"])
+    assert qkv.shape == (64 + 32 + 32, 64)
+    st.master_view("model.layers.0.self_attn.k_proj.weight").fill_(3.0)
+    assert (qkv[64:96] == 3.0).all()
+    assert list(m.state_dict().keys()) == [n for n, _ in c.param_shapes()]
+
+
+def test_activation_checkpointing_same_grads():
+    c = LlamaConfig.from_dict(dict(hidden_size=32, intermediate_size=64, num_attention_heads=2,
+                                   num_hidden_layers=2, vocab_size=50))
+    ids = torch.randint(0, 50, (2, 16))
+    m1 = LlamaForCausalLM(c).init_weights(0)
+    m1(ids, labels=ids).loss.backward()
+    m2 = LlamaForCausalLM(c, activation_checkpointing=True).init_weights(0)
+    m2(ids, labels=ids).loss.backward()
+    assert torch.allclose(m1.store.grad, m2.store.grad, atol=1e-7)
