@@ -26,6 +26,7 @@
 // Causal: tiles past the diagonal are never loaded; fully masked (wave, tile) pairs are skipped;
 // the longest query / key blocks are dispatched first.
 #include "common.h"
+#include <type_traits>
 
 using namespace nd;
 
@@ -86,6 +87,36 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16_t* tile, int rbase, int cba
   return cat4(tr_read(&tile[soff<HD>(row, col)]), tr_read(&tile[soff<HD>(row + 8, col)]));
 }
 
+// Rotate 8 (x1, x2) pairs held as two bf16x8 chunks: x1' = x1 c - x2 s, x2' = x2 c + x1 s
+// (sgn = -1 applies the inverse rotation).  fp32 math, one rounding, same as nd_rope_inplace.
+__device__ __forceinline__ void rope8(bf16x8& x1, bf16x8& x2, float4 c0, float4 c1, float4 s0, float4 s1, float sgn) {
+  const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const float a0 = bf2f((bf16_t)x1[j]), a1 = bf2f((bf16_t)x1[j + 1]);
+    const float b0 = bf2f((bf16_t)x2[j]), b1 = bf2f((bf16_t)x2[j + 1]);
+    const float s0_ = sgn * ss[j], s1_ = sgn * ss[j + 1];
+    const uint32_t u = pack2(a0 * cc[j] - b0 * s0_, a1 * cc[j + 1] - b1 * s1_);
+    const uint32_t v = pack2(b0 * cc[j] + a0 * s0_, b1 * cc[j + 1] + a1 * s1_);
+    x1[j] = (short)(u & 0xffff); x1[j + 1] = (short)(u >> 16);
+    x2[j] = (short)(v & 0xffff); x2[j + 1] = (short)(v >> 16);
+  }
+}
+
+// RoPE on register fragments f[t] = row[16t + 8h .. +7] (pairs t <-> t + NT/2, same lane).
+template <int HD>
+__device__ __forceinline__ void rope_frags(bf16x8* f, const float* cosT, const float* sinT, int pos, int h) {
+  constexpr int NT = HD / 16;
+#pragma unroll
+  for (int t = 0; t < NT / 2; ++t) {
+    const int d = 16 * t + 8 * h;
+    const float4* cp = reinterpret_cast<const float4*>(cosT + (int64_t)pos * HD + d);
+    const float4* sp = reinterpret_cast<const float4*>(sinT + (int64_t)pos * HD + d);
+    rope8(f[t], f[t + NT / 2], cp[0], cp[1], sp[0], sp[1], 1.f);
+  }
+}
+
 // Register-staged tile loader: ROWS x HD bf16 tile, 16-B chunks spread over 256 threads.
 template <int ROWS, int HD>
 struct Stage {
@@ -113,12 +144,100 @@ struct Stage {
   }
 };
 
+// Register-staged tile loader that applies RoPE (half-split rotation) on the fly: each thread owns
+// a (chunk, chunk + HD/16) pair of one row, so both halves of every rotated pair are in its
+// registers; cos/sin rows of the tile's positions come from the fp32 [T, HD] tables (L2-resident).
+template <int ROWS, int HD>
+struct StageRope {
+  static constexpr int CPR = HD / 8, HP = CPR / 2;
+  static constexpr int N = (ROWS * HP + 255) / 256;
+  bf16x8 a[N], b[N];
+  float4 c0[N], c1[N], s0[N], s1[N];
+  __device__ __forceinline__ void load(const bf16_t* base, int64_t stride, int row0, int nrows_valid,
+                                       const float* cosT, const float* sinT) {
+#pragma unroll
+    for (int it = 0; it < N; ++it) {
+      const int p = threadIdx.x + it * 256;
+      const int row = p / HP, ch = p % HP, pos = row0 + row;
+      a[it] = zero8();
+      b[it] = zero8();
+      c0[it] = c1[it] = s0[it] = s1[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p < ROWS * HP && pos < nrows_valid) {
+        a[it] = load16(base + (int64_t)pos * stride + ch * 8);
+        b[it] = load16(base + (int64_t)pos * stride + (ch + HP) * 8);
+        const float4* cp = reinterpret_cast<const float4*>(cosT + (int64_t)pos * HD + ch * 8);
+        const float4* sp = reinterpret_cast<const float4*>(sinT + (int64_t)pos * HD + ch * 8);
+        c0[it] = cp[0]; c1[it] = cp[1]; s0[it] = sp[0]; s1[it] = sp[1];
+      }
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* tile) const {
+#pragma unroll
+    for (int it = 0; it < N; ++it) {
+      const int p = threadIdx.x + it * 256;
+      if (p < ROWS * HP) {
+        const int row = p / HP, ch = p % HP;
+        bf16x8 ra = a[it], rb = b[it];
+        rope8(ra, rb, c0[it], c1[it], s0[it], s1[it], 1.f);
+        *reinterpret_cast<bf16x8*>(&tile[soff<HD>(row, ch * 8)]) = ra;
+        *reinterpret_cast<bf16x8*>(&tile[soff<HD>(row, (ch + HP) * 8)]) = rb;
+      }
+    }
+  }
+};
+
+template <bool ROPE, class S>
+__device__ __forceinline__ void load_tile(S& st, const bf16_t* base, int64_t stride, int row0, int nvalid,
+                                          const float* cosT, const float* sinT) {
+  if constexpr (ROPE) st.load(base, stride, row0, nvalid, cosT, sinT);
+  else st.load(base, stride, row0, nvalid);
+}
+
 constexpr float LOG2E = 1.4426950408889634f;
 
 // Store a [HD x 32] transposed accumulator (rows = head dim in registers, col = row index on the
-// lane) as 8-B packed bf16 groups into row `r` of a row-major output.
-template <int NO>
-__device__ __forceinline__ void store_T(bf16_t* out_row, const f32x16* acc, float mul, int h) {
+// lane) as 8-B packed bf16 groups into row `out_row`.  With tables, the inverse RoPE rotation is
+// applied first: head-dim rows d and d + HD/2 sit in the same lane (o <-> o + NO/2, or register
+// r <-> r + 8 when HD = 32), so the un-rotation is lane-local.
+template <int HD>
+__device__ __forceinline__ void store_T(bf16_t* out_row, f32x16* acc, float mul, int h, const float* cosT,
+                                        const float* sinT, int pos) {
+  constexpr int NO = HD / 32;
+  if (cosT) {
+    const float* cr = cosT + (int64_t)pos * HD;
+    const float* sr = sinT + (int64_t)pos * HD;
+    if (NO >= 2) {
+#pragma unroll
+      for (int o = 0; o < NO / 2; ++o)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d = o * 32 + 8 * g4 + 4 * h;
+          const float4 c = *reinterpret_cast<const float4*>(cr + d);
+          const float4 sn = *reinterpret_cast<const float4*>(sr + d);
+          const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float y1 = acc[o][4 * g4 + q], y2 = acc[o + NO / 2][4 * g4 + q];
+            acc[o][4 * g4 + q] = y1 * cc[q] + y2 * ss[q];
+            acc[o + NO / 2][4 * g4 + q] = y2 * cc[q] - y1 * ss[q];
+          }
+        }
+    } else {
+#pragma unroll
+      for (int g4 = 0; g4 < 2; ++g4) {
+        const int d = 8 * g4 + 4 * h;
+        const float4 c = *reinterpret_cast<const float4*>(cr + d);
+        const float4 sn = *reinterpret_cast<const float4*>(sr + d);
+        const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float y1 = acc[0][4 * g4 + q], y2 = acc[0][4 * g4 + 8 + q];
+          acc[0][4 * g4 + q] = y1 * cc[q] + y2 * ss[q];
+          acc[0][4 * g4 + 8 + q] = y2 * cc[q] - y1 * ss[q];
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int o = 0; o < NO; ++o)
 #pragma unroll
@@ -131,11 +250,12 @@ __device__ __forceinline__ void store_T(bf16_t* out_row, const f32x16* acc, floa
 }
 
 // =============================================================================== forward
-template <int HD>
+template <int HD, bool ROPE>
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int nh, int nkv, int T,
-                                                          int64_t ld, int64_t ldo, float scale) {
+                                                          int64_t ld, int64_t ldo, float scale,
+                                                          const float* __restrict__ cosT, const float* __restrict__ sinT) {
   constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[BN * HD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[BN * HD];
@@ -155,14 +275,16 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_fwd_kernel(cons
   bf16x8 qf[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) qf[t] = qi < T ? load16(Qb + (int64_t)qi * ld + 16 * t + 8 * h) : zero8();
+  if (ROPE && qi < T) rope_frags<HD>(qf, cosT, sinT, qi, h);
   f32x16 oacc[NO];
 #pragma unroll
   for (int o = 0; o < NO; ++o) oacc[o] = f32x16{};
   float m = -INFINITY, l = 0.f;
 
   const int ntiles = (min(T, qb * 128 + 128) + BN - 1) / BN;
-  Stage<BN, HD> sk, sv;
-  sk.load(Kb, ld, 0, T);
+  typename std::conditional<ROPE, StageRope<BN, HD>, Stage<BN, HD>>::type sk;
+  Stage<BN, HD> sv;
+  load_tile<ROPE>(sk, Kb, ld, 0, T, cosT, sinT);
   sv.load(Vb, ld, 0, T);
   for (int j = 0; j < ntiles; ++j) {
     const int k0 = j * BN;
@@ -171,7 +293,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_fwd_kernel(cons
     sv.store(Vs);
     __syncthreads();
     if (j + 1 < ntiles) {  // prefetch the next tile; its latency hides under this tile's MFMAs
-      sk.load(Kb, ld, k0 + BN, T);
+      load_tile<ROPE>(sk, Kb, ld, k0 + BN, T, cosT, sinT);
       sv.load(Vb, ld, k0 + BN, T);
     }
     if (k0 > q0w + 31) continue;  // whole tile above this wave's diagonal (wave-uniform)
@@ -225,7 +347,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_fwd_kernel(cons
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   if (qi < T) {
-    store_T<NO>(O + ((int64_t)b * T + qi) * ldo + (int64_t)head * HD, oacc, inv, h);
+    store_T<HD>(O + ((int64_t)b * T + qi) * ldo + (int64_t)head * HD, oacc, inv, h, nullptr, nullptr, 0);
     if (h == 0) LSE[((int64_t)b * nh + head) * T + qi] = m + log2f(lt);
   }
 }
@@ -261,12 +383,13 @@ __global__ void __launch_bounds__(256) attn_bwd_pre_kernel(const bf16_t* __restr
 }
 
 // dQ: per 128 queries of one (b, head), streaming 64-key K/V tiles up to the diagonal.
-template <int HD>
+template <int HD, bool ROPE, bool ROPE_OUT>
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                              const bf16_t* __restrict__ V, const bf16_t* __restrict__ dO,
                                                              const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                              bf16_t* __restrict__ dQ, int B, int nh, int nkv, int T,
-                                                             int64_t ld, int64_t ldo, float scale) {
+                                                             int64_t ld, int64_t ldo, float scale,
+                                                             const float* __restrict__ cosT, const float* __restrict__ sinT) {
   constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[BN * HD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[BN * HD];
@@ -290,6 +413,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
     qf[t] = qi < T ? load16(Qb + (int64_t)qi * ld + 16 * t + 8 * h) : zero8();
     dof[t] = qi < T ? load16(dOb + (int64_t)qi * ldo + 16 * t + 8 * h) : zero8();
   }
+  if (ROPE && qi < T) rope_frags<HD>(qf, cosT, sinT, qi, h);
   const int64_t rowstat = ((int64_t)b * nh + head) * T;
   const float lse = qi < T ? LSE[rowstat + qi] : 0.f;
   const float dlt = qi < T ? DELTA[rowstat + qi] : 0.f;
@@ -298,8 +422,9 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
   for (int o = 0; o < NO; ++o) dq[o] = f32x16{};
 
   const int ntiles = (min(T, qb * 128 + 128) + BN - 1) / BN;
-  Stage<BN, HD> sk, sv;
-  sk.load(Kb, ld, 0, T);
+  typename std::conditional<ROPE, StageRope<BN, HD>, Stage<BN, HD>>::type sk;
+  Stage<BN, HD> sv;
+  load_tile<ROPE>(sk, Kb, ld, 0, T, cosT, sinT);
   sv.load(Vb, ld, 0, T);
   for (int j = 0; j < ntiles; ++j) {
     const int k0 = j * BN;
@@ -308,7 +433,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
     sv.store(Vs);
     __syncthreads();
     if (j + 1 < ntiles) {
-      sk.load(Kb, ld, k0 + BN, T);
+      load_tile<ROPE>(sk, Kb, ld, k0 + BN, T, cosT, sinT);
       sv.load(Vb, ld, k0 + BN, T);
     }
     if (k0 > q0w + 31) continue;
@@ -341,18 +466,21 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
         for (int o = 0; o < NO; ++o) dq[o] = mfma32(tr_frag<HD>(Ks, kt * 32 + 16 * sidx, o * 32, g, i16), dsf, dq[o]);
       }
   }
-  if (qi < T) store_T<NO>(dQ + ((int64_t)b * T + qi) * ld + (int64_t)head * HD, dq, scale, h);
+  if (qi < T)
+    store_T<HD>(dQ + ((int64_t)b * T + qi) * ld + (int64_t)head * HD, dq, scale, h, ROPE_OUT ? cosT : nullptr, sinT, qi);
 }
 
 // dK, dV: per 128 keys of one (b, kv head); loops over the GQA group's query heads and 64-query
 // tiles from the diagonal to T.
-template <int HD>
+template <int HD, bool ROPE, bool ROPE_OUT>
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                                const bf16_t* __restrict__ V, const bf16_t* __restrict__ dO,
                                                                const float* __restrict__ LSE,
                                                                const float* __restrict__ DELTA, bf16_t* __restrict__ dK,
                                                                bf16_t* __restrict__ dV, int B, int nh, int nkv, int T,
-                                                               int64_t ld, int64_t ldo, float scale) {
+                                                               int64_t ld, int64_t ldo, float scale,
+                                                               const float* __restrict__ cosT,
+                                                               const float* __restrict__ sinT) {
   constexpr int BQ = 64, NT = HD / 16, NO = HD / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * HD];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * HD];
@@ -377,6 +505,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
     kf[t] = key < T ? load16(Kb + (int64_t)key * ld + 16 * t + 8 * h) : zero8();
     vf[t] = key < T ? load16(Vb + (int64_t)key * ld + 16 * t + 8 * h) : zero8();
   }
+  if (ROPE && key < T) rope_frags<HD>(kf, cosT, sinT, key, h);
   f32x16 dk[NO], dv[NO];
 #pragma unroll
   for (int o = 0; o < NO; ++o) { dk[o] = f32x16{}; dv[o] = f32x16{}; }
@@ -384,12 +513,13 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
   const int qstart = (kb * 128) / BQ * BQ;
   const int ntq = (T - qstart + BQ - 1) / BQ;
   const int nit = ntq * rep;
-  Stage<BQ, HD> sq, sd;
+  typename std::conditional<ROPE, StageRope<BQ, HD>, Stage<BQ, HD>>::type sq;
+  Stage<BQ, HD> sd;
   float lse_n = 0.f, del_n = 0.f;
   auto prefetch = [&](int it) {
     const int head = kvh * rep + it / ntq;
     const int q0 = qstart + (it % ntq) * BQ;
-    sq.load(Q + (int64_t)b * T * ld + (int64_t)head * HD, ld, q0, T);
+    load_tile<ROPE>(sq, Q + (int64_t)b * T * ld + (int64_t)head * HD, ld, q0, T, cosT, sinT);
     sd.load(dO + (int64_t)b * T * ldo + (int64_t)head * HD, ldo, q0, T);
     if (threadIdx.x < BQ) {
       const int qq = q0 + threadIdx.x;
@@ -447,29 +577,36 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
     }
   }
   if (key < T) {
-    store_T<NO>(dK + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dk, scale, h);
-    store_T<NO>(dV + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dv, 1.f, h);
+    store_T<HD>(dK + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dk, scale, h, ROPE_OUT ? cosT : nullptr, sinT, key);
+    store_T<HD>(dV + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dv, 1.f, h, nullptr, nullptr, 0);
   }
 }
 
 // ------------------------------------------------------------------------------------ launchers
 template <int HD>
 static int fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, int B, int nh, int nkv, int T,
-                      int64_t ld, int64_t ldo, float scale, hipStream_t s) {
+                      int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, hipStream_t s) {
   const int nqb = (T + 127) / 128;
-  hipLaunchKernelGGL(attn_fwd_kernel<HD>, dim3(nqb * B * nh), dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k,
-                     (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale);
+  const dim3 g(nqb * B * nh), b(256);
+  if (cosT)
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, true>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                       (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, false>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                       (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
   ND_LAUNCH_CHECK();
 }
 
+// cosT/sinT: fp32 [T, hd] RoPE tables (nullptr = q/k already rotated).  q/k/v are then the RAW
+// projection outputs and the kernel rotates q and k on load.
 ND_API int nd_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int nh, int nkv, int T,
-                       int hd, int64_t ld, int64_t ldo, int64_t /*reserved*/, int64_t /*reserved*/, float scale,
+                       int hd, int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale,
                        hipStream_t s) {
   if (nh % nkv || (ld % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
   switch (hd) {
-    case 32: return fwd_launch<32>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, scale, s);
-    case 64: return fwd_launch<64>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, scale, s);
-    case 128: return fwd_launch<128>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, scale, s);
+    case 32: return fwd_launch<32>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
+    case 64: return fwd_launch<64>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
+    case 128: return fwd_launch<128>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -487,29 +624,45 @@ ND_API int nd_attn_bwd_pre(const void* o, const void* dout, float* delta, int B,
   ND_LAUNCH_CHECK();
 }
 
+template <int HD, bool ROPE, bool ROPE_OUT>
+static void bwd_launch_t(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                         const float* delta, void* dq, void* dk, void* dv, int B, int nh, int nkv, int T, int64_t ld,
+                         int64_t ldo, const float* cosT, const float* sinT, float scale, hipStream_t s) {
+  const int nb = (T + 127) / 128;
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, ROPE, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, B,
+                     nh, nkv, T, ld, ldo, scale, cosT, sinT);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT>), dim3(nb * B * nh), dim3(256), 0, s, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, nh, nkv, T,
+                     ld, ldo, scale, cosT, sinT);
+}
+
+// rope_mode 0: no RoPE; 1: q/k are RAW projections -- rotated on load, dq/dk un-rotated on store;
+// 2: q/k were rotated in place before the forward -- only the dq/dk un-rotation (store epilogue).
 template <int HD>
 static int bwd_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse, const float* delta,
-                      void* dq, void* dk, void* dv, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
-                      hipStream_t s) {
-  const int nb = (T + 127) / 128;
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HD>, dim3(nb * B * nkv), dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k,
-                     (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld,
-                     ldo, scale);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<HD>, dim3(nb * B * nh), dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k,
-                     (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale);
+                      void* dq, void* dk, void* dv, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo,
+                      const float* cosT, const float* sinT, float scale, int rope_mode, hipStream_t s) {
+  if (rope_mode == 1)
+    bwd_launch_t<HD, true, true>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
+  else if (rope_mode == 2)
+    bwd_launch_t<HD, false, true>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
+  else
+    bwd_launch_t<HD, false, false>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
   ND_LAUNCH_CHECK();
 }
 
-// dq/dk/dv may point into one packed dqkv buffer (row stride ld).  `dqacc` is unused (kept for ABI).
+// dq/dk/dv may point into one packed dqkv buffer (row stride ld).
 ND_API int nd_attn_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
-                       const float* delta, void* dq, void* dk, void* dv, float* /*dqacc*/, int B, int nh, int nkv,
-                       int T, int hd, int64_t ld, int64_t ldo, int64_t /*reserved*/, int64_t /*reserved*/, float scale,
-                       void* /*reserved*/, hipStream_t s) {
+                       const float* delta, void* dq, void* dk, void* dv, float* /*unused*/, int B, int nh, int nkv,
+                       int T, int hd, int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale,
+                       int rope_mode, hipStream_t s) {
   if (nh % nkv || (ld % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
+  if (rope_mode && !(cosT && sinT)) return (int)hipErrorInvalidValue;
   switch (hd) {
-    case 32: return bwd_launch<32>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, scale, s);
-    case 64: return bwd_launch<64>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, scale, s);
-    case 128: return bwd_launch<128>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, scale, s);
+    case 32: return bwd_launch<32>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
+    case 64: return bwd_launch<64>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
+    case 128: return bwd_launch<128>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -1,0 +1,349 @@
+// Weight-gradient GEMM for gfx950:  C[M, N] (fp32) += A^T B,  A = dY [K, M], B = X [K, N]  (bf16, row-major)
+//
+// Why a custom kernel: in the wgrad product the reduction dimension K is the token axis, which is the
+// STRIDED axis of both operands as they come out of the forward / backward.  hipBLASLt runs this
+// "K-outer" layout at 330-900 TF/s on the Llama-150M shapes (vs 1.1-1.4 PF/s for fwd / dgrad), and
+// the tall-skinny shapes (M x N = 1024 x 1024 with K = 32768) give too few output tiles to fill
+// 256 CUs.  Here:
+//   * both operands are staged through LDS exactly as they sit in memory ([k][m] / [k][n] rows,
+//     16-B coalesced global loads) and the MFMA fragments (8 consecutive k of one m / n) are fetched
+//     with the gfx950 transposing read ds_read_b64_tr_b16 -- no transpose pass in HBM;
+//   * LDS rows are XOR-swizzled ((row & 3) << 2 on the 16-B chunk index) so the four rows one
+//     32-lane half reads land in four different quarters of the bank row (conflict-free);
+//   * split-K: when the output has few tiles, K is split over S workgroups writing fp32 slabs that a
+//     streaming kernel sums into C in a fixed order -- deterministic (no float atomics);
+//   * register-staged prefetch of the next 64-deep K tile is issued before the current tile's MFMAs;
+//   * XCD-aware block remap so the workgroups sharing an A row-panel run on one XCD's L2.
+// Tile: 128 x 128 per 256-thread workgroup (2 x 2 waves of 64 x 64, 2 x 2 v_mfma_f32_32x32x16_bf16).
+#include "common.h"
+
+using namespace nd;
+
+typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
+typedef short sv4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bfv8, a), __builtin_bit_cast(bfv8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ sv4 tr_read(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((sv4 __attribute__((address_space(3)))*)(p));
+}
+
+// [BK][128] bf16 tile, 256-B rows, 16-B chunk index XOR (row & 3) << 2.
+__device__ __forceinline__ int toff(int row, int col) {
+  return row * 128 + (((col >> 3) ^ ((row & 3) << 2)) << 3) + (col & 7);
+}
+
+// Fragment with k (tile rows) natural: element j of lane half h = row kbase + 8h + j, column cbase + (lane & 31).
+__device__ __forceinline__ bf16x8 frag(const bf16_t* tile, int kbase, int cbase, int g, int i) {
+  const int row = kbase + 8 * (g >> 1) + (i >> 2);
+  const int col = cbase + 16 * (g & 1) + 4 * (i & 3);
+  const sv4 lo = tr_read(&tile[toff(row, col)]);
+  const sv4 hi = tr_read(&tile[toff(row + 4, col)]);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+struct TileLoad {
+  static constexpr int N = (BK * 16) / 256;  // 16-B chunks per thread (4)
+  bf16x8 v[N];
+  __device__ __forceinline__ void load(const bf16_t* base, int64_t ld, int k0, int kend, int c0, int cols) {
+#pragma unroll
+    for (int it = 0; it < N; ++it) {
+      const int c = threadIdx.x + it * 256;
+      const int row = c >> 4, ch = c & 15;
+      const int k = k0 + row, col = c0 + ch * 8;
+      if (k < kend && col < cols) v[it] = *reinterpret_cast<const bf16x8*>(base + (int64_t)k * ld + col);
+      else v[it] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* tile) const {
+#pragma unroll
+    for (int it = 0; it < N; ++it) {
+      const int c = threadIdx.x + it * 256;
+      const int row = c >> 4, ch = c & 15;
+      *reinterpret_cast<bf16x8*>(&tile[toff(row, ch * 8)]) = v[it];
+    }
+  }
+};
+
+}  // namespace
+
+// grid = tiles * S;  S == 1: C += acc in place;  S > 1: slab[s][M][N] = acc.
+__global__ void __launch_bounds__(256, 2) wgrad_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                       float* __restrict__ C, float* __restrict__ slab, int M, int N,
+                                                       int K, int64_t lda, int64_t ldb, int64_t ldc, int S, int kchunk) {
+  __shared__ __attribute__((aligned(16))) bf16_t As[BK * BM];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[BK * BN];
+  const int tn_count = (N + BN - 1) / BN;
+  const int tiles = ((M + BM - 1) / BM) * tn_count;
+  const int id = xcd_remap(blockIdx.x, tiles * S);
+  const int tile = id / S, split = id % S;
+  const int m0 = (tile / tn_count) * BM, n0 = (tile % tn_count) * BN;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int wm = w >> 1, wn = w & 1;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+
+  TileLoad la, lb;
+  la.load(A, lda, kbeg, kend, m0, M);
+  lb.load(B, ldb, kbeg, kend, n0, N);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+    la.store(As);
+    lb.store(Bs);
+    __syncthreads();
+    if (k0 + BK < kend) {
+      la.load(A, lda, k0 + BK, kend, m0, M);
+      lb.load(B, ldb, k0 + BK, kend, n0, N);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) fa[a] = frag(As, ks * 16, wm * 64 + a * 32, g, i16);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) fb[b] = frag(Bs, ks * 16, wn * 64 + b * 32, g, i16);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(fa[a], fb[b], acc[a][b]);
+    }
+  }
+  // epilogue: row m = m0 + wm*64 + a*32 + (r&3) + 8(r>>2) + 4h ; col n = n0 + wn*64 + b*32 + c32
+  float* out = S == 1 ? C : slab + (int64_t)split * M * N;
+  const int64_t ldo = S == 1 ? ldc : N;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int n = n0 + wn * 64 + b * 32 + c32;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M) {
+          float* p = out + (int64_t)m * ldo + n;
+          if (S == 1) *p += acc[a][b][r];
+          else *p = acc[a][b][r];
+        }
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Large-tile variant: 256 x 256 per 512-thread workgroup (8 waves as 2 (M) x 4 (N), 128 x 64 each =
+// 4 x 2 MFMA tiles), BK = 32, DOUBLE-BUFFERED LDS with one barrier per K tile:
+//   compute(buf[k&1]) | global loads of tile k+2 in flight | write tile k+1 regs -> buf[(k+1)&1] | barrier
+// 1.5 transposing LDS reads per MFMA (vs 2 in the 128 x 128 kernel), 16 MFMAs per wave per barrier.
+namespace {
+constexpr int BM2 = 256, BN2 = 256, BK2 = 32;
+
+// [BK2][256] bf16 tile, 512-B rows: 16-B chunk index XOR ((row & 3) << 2) -> the four rows a 32-lane
+// half reads with ds_read_b64_tr_b16 fall in different quarters of the 256-B bank row.
+__device__ __forceinline__ int toff2(int row, int col) {
+  return row * 256 + (((col >> 3) ^ ((row & 3) << 2)) << 3) + (col & 7);
+}
+
+__device__ __forceinline__ bf16x8 frag2(const bf16_t* tile, int kbase, int cbase, int g, int i) {
+  const int row = kbase + 8 * (g >> 1) + (i >> 2);
+  const int col = cbase + 16 * (g & 1) + 4 * (i & 3);
+  const sv4 lo = tr_read(&tile[toff2(row, col)]);
+  const sv4 hi = tr_read(&tile[toff2(row + 4, col)]);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+struct TileLoad2 {  // BK2 x 256 bf16 = 1024 16-B chunks over 512 threads
+  bf16x8 v[2];
+  __device__ __forceinline__ void load(const bf16_t* base, int64_t ld, int k0, int kend, int c0, int cols) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int c = threadIdx.x + it * 512;
+      const int row = c >> 5, ch = c & 31;
+      const int k = k0 + row, col = c0 + ch * 8;
+      if (k < kend && col < cols) v[it] = *reinterpret_cast<const bf16x8*>(base + (int64_t)k * ld + col);
+      else v[it] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* tile) const {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int c = threadIdx.x + it * 512;
+      const int row = c >> 5, ch = c & 31;
+      *reinterpret_cast<bf16x8*>(&tile[toff2(row, ch * 8)]) = v[it];
+    }
+  }
+};
+}  // namespace
+
+__global__ void __launch_bounds__(512, 2) wgrad256_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                          float* __restrict__ C, float* __restrict__ slab, int M, int N,
+                                                          int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
+                                                          int kchunk) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* As[2] = {smem, smem + BK2 * BM2};
+  bf16_t* Bs[2] = {smem + 2 * BK2 * BM2, smem + 2 * BK2 * BM2 + BK2 * BN2};
+  const int tn_count = (N + BN2 - 1) / BN2;
+  const int tiles = ((M + BM2 - 1) / BM2) * tn_count;
+  const int id = xcd_remap(blockIdx.x, tiles * S);
+  const int tile = id / S, split = id % S;
+  const int m0 = (tile / tn_count) * BM2, n0 = (tile % tn_count) * BN2;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int wm = w >> 2, wn = w & 3;  // 2 x 4 waves, wave tile 128 (M) x 64 (N)
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+
+  const int nk = (kend - kbeg + BK2 - 1) / BK2;
+  TileLoad2 la, lb;
+  if (nk > 0) {
+    la.load(A, lda, kbeg, kend, m0, M);
+    lb.load(B, ldb, kbeg, kend, n0, N);
+    la.store(As[0]);
+    lb.store(Bs[0]);
+  }
+  __syncthreads();
+  if (nk > 1) {
+    la.load(A, lda, kbeg + BK2, kend, m0, M);
+    lb.load(B, ldb, kbeg + BK2, kend, n0, N);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16_t* a_t = As[kt & 1];
+    const bf16_t* b_t = Bs[kt & 1];
+#pragma unroll
+    for (int ks = 0; ks < BK2 / 16; ++ks) {
+      bf16x8 fb[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) fb[b] = frag2(b_t, ks * 16, wn * 64 + b * 32, g, i16);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const bf16x8 fa = frag2(a_t, ks * 16, wm * 128 + a * 32, g, i16);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(fa, fb[b], acc[a][b]);
+      }
+    }
+    if (kt + 1 < nk) {
+      la.store(As[(kt + 1) & 1]);
+      lb.store(Bs[(kt + 1) & 1]);
+    }
+    __syncthreads();
+    if (kt + 2 < nk) {
+      la.load(A, lda, kbeg + (kt + 2) * BK2, kend, m0, M);
+      lb.load(B, ldb, kbeg + (kt + 2) * BK2, kend, n0, N);
+    }
+  }
+  float* out = S == 1 ? C : slab + (int64_t)split * M * N;
+  const int64_t ldo = S == 1 ? ldc : N;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int n = n0 + wn * 64 + b * 32 + c32;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M) {
+          float* p = out + (int64_t)m * ldo + n;
+          if (S == 1) *p += acc[a][b][r];
+          else *p = acc[a][b][r];
+        }
+      }
+    }
+}
+
+// C[m][n] += sum_s slab[s][m][n]   (fixed summation order)
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ C, int M,
+                                                          int N, int64_t ldc, int S) {
+  const int64_t total4 = (int64_t)M * N / 4;
+  const int64_t plane = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total4; i += (int64_t)gridDim.x * 256) {
+    const int64_t e = i * 4;
+    const int m = (int)(e / N), n = (int)(e % N);
+    float4 s = *reinterpret_cast<const float4*>(slab + e);
+    for (int k = 1; k < S; ++k) {
+      const float4 t = *reinterpret_cast<const float4*>(slab + k * plane + e);
+      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    float4* cp = reinterpret_cast<float4*>(C + (int64_t)m * ldc + n);
+    float4 c = *cp;
+    c.x += s.x; c.y += s.y; c.z += s.z; c.w += s.w;
+    *cp = c;
+  }
+}
+
+static int splits_for(int tiles, int K, int bk, int target) {
+  int S = target / tiles;
+  if (S < 1) S = 1;
+  if (S > 16) S = 16;
+  while (S > 1 && K / S < 4 * bk) --S;
+  return S;
+}
+
+// Variant choice: the 256 x 256 kernel (1 workgroup / CU) when the output has >= 8 such tiles,
+// else the 128 x 128 kernel.  Returns splits * 2 + (large ? 1 : 0) so the caller can size the slab.
+static int plan(int M, int N, int K, int* S_out) {
+  const int t256 = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
+  if (t256 >= 8) {
+    *S_out = splits_for(t256, K, BK2, 256);
+    return 1;
+  }
+  const int t128 = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  *S_out = splits_for(t128, K, BK, 512);
+  return 0;
+}
+
+// Number of K splits for this shape (slab workspace = S * M * N floats when S > 1).
+ND_API int nd_wgrad_splits(int M, int N, int K) {
+  int S;
+  plan(M, N, K, &S);
+  return S;
+}
+
+// A: dY [K, M] (lda), B: X [K, N] (ldb), C: fp32 [M, N] (ldc).  M, N multiples of 8; any K.
+ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, int N, int K, int64_t lda, int64_t ldb,
+                    int64_t ldc, hipStream_t s) {
+  if (M % 8 || N % 8 || lda % 8 || ldb % 8 || (ldc % 4)) return (int)hipErrorInvalidValue;
+  int S;
+  const int large = plan(M, N, K, &S);
+  if (S > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
+  if (large) {
+    const int kchunk = ((K + S - 1) / S + BK2 - 1) / BK2 * BK2;
+    const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
+    const size_t lds = 2 * (size_t)BK2 * (BM2 + BN2) * sizeof(bf16_t);
+    hipLaunchKernelGGL(wgrad256_kernel, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B, C,
+                       slab, M, N, K, lda, ldb, ldc, S, kchunk);
+  } else {
+    const int kchunk = ((K + S - 1) / S + BK - 1) / BK * BK;
+    const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * S), dim3(256), 0, s, (const bf16_t*)A, (const bf16_t*)B, C, slab, M,
+                       N, K, lda, ldb, ldc, S, kchunk);
+  }
+  if (S > 1) {
+    int64_t blocks = ((int64_t)M * N / 4 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, slab, C, M, N, ldc, S);
+  }
+  ND_LAUNCH_CHECK();
+}

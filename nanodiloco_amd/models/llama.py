@@ -134,7 +134,8 @@ class LlamaForCausalLM:
         eps = c.rms_norm_eps
         qn = self._qkv_names[i]
         qkv = ops.linear(y, self._fused(qn, "shadow"), self._fused(qn, "grad"))
-        o = ops.attention(qkv, cos, sin, B, T, c.num_attention_heads, c.num_key_value_heads, c.head_dim)
+        o = ops.attention(qkv, cos, sin, B, T, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
+                          inplace=True)
         a = ops.linear(o, self._w(p + "self_attn.o_proj.weight"), self._g(p + "self_attn.o_proj.weight"))
         y, h = ops.add_rmsnorm(h, a, self._m(p + "post_attention_layernorm.weight"),
                                self._g(p + "post_attention_layernorm.weight"), eps, cdt)

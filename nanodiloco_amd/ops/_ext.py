@@ -107,9 +107,9 @@ def _declare(L: ctypes.CDLL):
         # rope (in place on packed qkv)
         "nd_rope_inplace": [P, I, P, P, L64, I, I, I, I, I, I, P],
         # attention
-        "nd_attn_fwd": [P, P, P, P, P, I, I, I, I, I, L64, L64, L64, L64, F, P],
+        "nd_attn_fwd": [P, P, P, P, P, I, I, I, I, I, L64, L64, P, P, F, P],
         "nd_attn_bwd_pre": [P, P, P, I, I, I, L64, L64, P],
-        "nd_attn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, L64, L64, L64, L64, F, P, P],
+        "nd_attn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, L64, L64, P, P, F, I, P],
         # mlp
         "nd_swiglu_fwd": [P, P, I, L64, I, P],
         "nd_swiglu_bwd": [P, P, P, I, L64, I, P],
@@ -124,6 +124,9 @@ def _declare(L: ctypes.CDLL):
         "nd_pseudograd": [P, P, P, I, L64, P],
         "nd_outer_nesterov": [P, P, P, I, P, P, I, L64, F, F, F, I, P, P, P],
         "nd_axpby": [P, P, L64, F, F, P],
+        # weight-gradient GEMM
+        "nd_wgrad_splits": [I, I, I],
+        "nd_wgrad": [P, P, P, P, I, I, I, L64, L64, L64, P],
     }
     for name, argtypes in sigs.items():
         fn = getattr(L, name, None)

@@ -5,12 +5,12 @@ packed).  The HIP path never transposes to ``[B, H, T, hd]``: the attention kern
 (batch, head, token) strides and read 128-B head rows straight out of the packed buffer, and
 write ``O`` as ``[B*T, nh*hd]`` -- exactly the o_proj GEMM input.
 
-HIP path
-  fwd: ``nd_rope_inplace`` on a copy of q|k (half-split rotation, fp32 tables)
-       ``nd_attn_fwd``  -- MFMA flash attention, online softmax, saves LSE (fp32, log2 domain)
+HIP path (RoPE: q|k rotated in place by one streaming pass -- no copy; dq/dk are un-rotated inside the
+backward kernels' store epilogues, so the backward needs no extra pass)
+  fwd: ``nd_rope_inplace`` then ``nd_attn_fwd``  -- MFMA flash attention, online softmax, saves LSE (fp32, log2 domain)
   bwd: ``nd_attn_bwd_pre`` (delta = rowsum(dO * O)), ``nd_attn_bwd`` = a key-parallel dK/dV kernel
-       and a query-parallel dQ kernel (both recompute P from LSE; no atomics -> deterministic),
-       then ``nd_rope_inplace(inverse)`` on dq|dk.
+       and a query-parallel dQ kernel (both recompute P from LSE; no atomics -> deterministic).
+``nd_rope_inplace`` (stand-alone rotation kernel) remains available for other callers.
 GQA (nkv < nh) is handled by head-index mapping inside the kernels (no K/V repetition).
 """
 from __future__ import annotations
@@ -43,50 +43,57 @@ def _rope(qkv, cos, sin, B, T, nh, nkv, hd, inverse):
 
 
 class FlashAttnFn(torch.autograd.Function):
+    """RoPE is applied to q|k IN PLACE in the packed projection output (one streaming pass, no copy):
+    that buffer is this op's private input -- the projection's backward saved its input, not its
+    output -- and it is saved here only after the rotation.  The backward kernels un-rotate dq/dk in
+    their store epilogues (rope_mode 2), so the gradient returned is w.r.t. the raw projection."""
+
     @staticmethod
     def forward(ctx, qkv, cos, sin, B, T, nh, nkv, hd):
-        qkv_r = qkv.clone()
-        _rope(qkv_r, cos, sin, B, T, nh, nkv, hd, inverse=False)
-        ld = qkv_r.shape[1]
-        q = qkv_r
-        k = qkv_r[:, nh * hd:]
-        v = qkv_r[:, (nh + nkv) * hd:]
+        ld = qkv.shape[1]
+        _rope(qkv, cos, sin, B, T, nh, nkv, hd, inverse=False)
+        k = qkv[:, nh * hd:]
+        v = qkv[:, (nh + nkv) * hd:]
         o = torch.empty(B * T, nh * hd, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(B, nh, T, dtype=torch.float32, device=qkv.device)
-        scale = hd ** -0.5
         L = _ext.lib()
-        _ext.check(L.nd_attn_fwd(_ext.ptr(q), _ext.ptr(k), _ext.ptr(v), _ext.ptr(o), _ext.ptr(lse),
-                                 B, nh, nkv, T, hd, ld, nh * hd, 0, 0, float(scale), _ext.stream_ptr(qkv.device)),
-                   "nd_attn_fwd")
-        ctx.save_for_backward(qkv_r, o, lse, cos, sin)
+        _ext.check(L.nd_attn_fwd(_ext.ptr(qkv), _ext.ptr(k), _ext.ptr(v), _ext.ptr(o), _ext.ptr(lse),
+                                 B, nh, nkv, T, hd, ld, nh * hd, 0, 0, float(hd ** -0.5),
+                                 _ext.stream_ptr(qkv.device)), "nd_attn_fwd")
+        ctx.save_for_backward(qkv, o, lse, cos, sin)
         ctx.dims = (B, T, nh, nkv, hd)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv_r, o, lse, cos, sin = ctx.saved_tensors
+        qkv, o, lse, cos, sin = ctx.saved_tensors
         B, T, nh, nkv, hd = ctx.dims
         do = do.contiguous()
-        ld = qkv_r.shape[1]
+        ld = qkv.shape[1]
         L = _ext.lib()
         dev = do.device
         delta = torch.empty(B, nh, T, dtype=torch.float32, device=dev)
         _ext.check(L.nd_attn_bwd_pre(_ext.ptr(o), _ext.ptr(do), _ext.ptr(delta), B, nh, T, hd, nh * hd,
                                      _ext.stream_ptr(dev)), "nd_attn_bwd_pre")
-        dqkv = torch.empty_like(qkv_r)
-        q, k, v = qkv_r, qkv_r[:, nh * hd:], qkv_r[:, (nh + nkv) * hd:]
-        dq, dk, dv = dqkv, dqkv[:, nh * hd:], dqkv[:, (nh + nkv) * hd:]
-        _ext.check(L.nd_attn_bwd(_ext.ptr(q), _ext.ptr(k), _ext.ptr(v), _ext.ptr(do), _ext.ptr(lse), _ext.ptr(delta),
-                                 _ext.ptr(dq), _ext.ptr(dk), _ext.ptr(dv), 0,
-                                 B, nh, nkv, T, hd, ld, nh * hd, 0, 0, float(hd ** -0.5), 0,
+        dqkv = torch.empty_like(qkv)
+        k, v = qkv[:, nh * hd:], qkv[:, (nh + nkv) * hd:]
+        dk, dv = dqkv[:, nh * hd:], dqkv[:, (nh + nkv) * hd:]
+        _ext.check(L.nd_attn_bwd(_ext.ptr(qkv), _ext.ptr(k), _ext.ptr(v), _ext.ptr(do), _ext.ptr(lse), _ext.ptr(delta),
+                                 _ext.ptr(dqkv), _ext.ptr(dk), _ext.ptr(dv), 0,
+                                 B, nh, nkv, T, hd, ld, nh * hd, _ext.ptr(cos), _ext.ptr(sin), float(hd ** -0.5), 2,
                                  _ext.stream_ptr(dev)), "nd_attn_bwd")
-        _rope(dqkv, cos, sin, B, T, nh, nkv, hd, inverse=True)
         return dqkv, None, None, None, None, None, None, None
 
 
 def attention(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, B: int, T: int, nh: int, nkv: int,
-              hd: int) -> torch.Tensor:
-    """Causal self-attention with RoPE; qkv [B*T, (nh+2nkv)*hd] -> [B*T, nh*hd]."""
+              hd: int, inplace: bool = False) -> torch.Tensor:
+    """Causal self-attention with RoPE; qkv [B*T, (nh+2nkv)*hd] -> [B*T, nh*hd].
+
+    ``inplace=True`` lets the HIP path rotate q|k inside ``qkv`` itself (the model passes it for the
+    projection output it owns); otherwise a private copy is rotated."""
     if _ext.use_hip(qkv):
-        return FlashAttnFn.apply(qkv.contiguous(), cos, sin, B, T, nh, nkv, hd)
+        x = qkv.contiguous()
+        if not inplace and x.data_ptr() == qkv.data_ptr():
+            x = x.clone()  # never rotate a caller-visible tensor
+        return FlashAttnFn.apply(x, cos, sin, B, T, nh, nkv, hd)
     return ref.attention_block(qkv, cos, sin, B, T, nh, nkv, hd, use_sdpa=True)

@@ -3,13 +3,16 @@
 ``y = x @ W^T`` for W of shape [out, in].  Forward and dgrad are plain library GEMMs
 (hipBLASLt through ``torch.mm``).  The weight gradient is accumulated straight into the fp32
 ``ParamStore.grad`` view: bf16 operands, fp32 accumulate, beta=1 -- one GEMM, no bf16 grad
-tensor, no separate accumulate pass (this replaces autograd's per-parameter AccumulateGrad,
+tensor, no separate accumulate pass.  On the HIP path that GEMM is our own ``nd_wgrad`` kernel
+(ops/gemm.py); otherwise hipBLASLt ``addmm(out_dtype=fp32)`` (this replaces autograd's per-parameter AccumulateGrad,
 K11 in SURVEY.md §2.3).  Fused weights (q|k|v, gate|up) are single views, so one GEMM covers
 all three / both projections.
 """
 from __future__ import annotations
 
 import torch
+
+from . import _ext
 
 _DTYPE_OUT_OK = {"checked": False, "ok": False}
 
@@ -19,6 +22,11 @@ def wgrad_accumulate(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor):
     if dy.dtype == torch.float32:
         gw.addmm_(dy.t(), x)
         return
+    if gw.is_cuda and _ext.get_backend() != "torch":
+        from .gemm import wgrad, wgrad_supported
+        if wgrad_supported(gw, dy, x):
+            wgrad(gw, dy, x)
+            return
     if gw.is_cuda:
         st = _DTYPE_OUT_OK
         if not st["checked"] or st["ok"]:

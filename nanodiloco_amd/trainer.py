@@ -27,6 +27,7 @@ from .parallel.diloco import Diloco
 from .parallel.dist import DistEnv, init_distributed
 from .parallel.inner_ddp import InnerGradSync
 from .utils.logging import make_sink
+from .utils.profiling import PhaseTimer, torch_profile
 from .utils.run_name import create_run_name
 from .utils.seed import set_seed_all
 
@@ -73,6 +74,9 @@ class TrainArgs:
     tokenizer: str = "huggyllama/llama-7b"
     debug_checks: bool = False
     mask_pad_labels: bool = True
+    phase_timing: bool = True      # HIP-event timing of fwd+bwd / inner optimizer / outer step (logged)
+    profile_dir: Optional[str] = None   # torch.profiler Chrome trace of `profile_steps` steps
+    profile_steps: int = 0
 
 
 def _dtype(name: str, device: torch.device) -> torch.dtype:
@@ -136,6 +140,7 @@ class Trainer:
                 except Exception:
                     pass
         self.run_name = create_run_name("nanodiloco", self.run_config, is_debug=False)
+        self.timer = PhaseTimer(a.phase_timing)
         self.sink = make_sink(e.rank, a.project, self.run_name, {**self.run_config, **dataclasses.asdict(a)},
                               jsonl_path=a.log_file, use_wandb=a.wandb)
 
@@ -143,16 +148,18 @@ class Trainer:
     def inner_step(self) -> torch.Tensor:
         """grad_accum micro-batches fwd+bwd, inner-DDP sync, clip+AdamW. Returns mean loss (device)."""
         loss_sum = None
-        for micro in range(self.grad_accum):
-            batch = next(self.data)
-            if micro == self.grad_accum - 1:
-                self.inner_sync.arm()
-            out = self.model(batch["input_ids"], labels=batch["labels"], loss_scale=self.loss_scale)
-            out.loss.backward()
-            l = out.loss.detach()
-            loss_sum = l if loss_sum is None else loss_sum + l
-        self.inner_sync.finish()
-        self.diloco.inner_step()
+        with self.timer.phase("fwd_bwd"):
+            for micro in range(self.grad_accum):
+                batch = next(self.data)
+                if micro == self.grad_accum - 1:
+                    self.inner_sync.arm()
+                out = self.model(batch["input_ids"], labels=batch["labels"], loss_scale=self.loss_scale)
+                out.loss.backward()
+                l = out.loss.detach()
+                loss_sum = l if loss_sum is None else loss_sum + l
+        with self.timer.phase("inner_opt"):
+            self.inner_sync.finish()
+            self.diloco.inner_step()
         return loss_sum / self.grad_accum
 
     def train(self) -> Dict[str, Any]:
@@ -161,12 +168,21 @@ class Trainer:
         tokens_per_step = a.batch_size * a.seq_length
         last_t, last_step = time.perf_counter(), self.start_step
         last_loss = float("nan")
+        prof_at = self.start_step + 2 if (a.profile_dir and a.profile_steps) else -1
+        prof_ctx = None
         for step in range(self.start_step, a.total_steps):
+            if step == prof_at:
+                prof_ctx = torch_profile(a.profile_dir, e.rank)
+                prof_ctx.__enter__()
             loss = self.inner_step()
             real_step = step + 1
             did_outer = real_step % a.inner_steps == 0
             if did_outer:
-                self.diloco.outer_step()
+                with self.timer.phase("outer"):
+                    self.diloco.outer_step()
+            if prof_ctx is not None and step + 1 >= prof_at + a.profile_steps:
+                prof_ctx.__exit__(None, None, None)
+                prof_ctx = None
             if (a.log_every and real_step % a.log_every == 0) or real_step == a.total_steps:
                 lv = float(loss.item())
                 now = time.perf_counter()
@@ -187,6 +203,8 @@ class Trainer:
                 if did_outer:
                     metrics["bytes_outer"] = self.diloco.bytes_per_outer_step
                     metrics["sync_s"] = self.diloco.avg_sync_time
+                    metrics["comm_ms"] = self.diloco.comm_ms()
+                metrics.update(self.timer.report())
                 self.sink.log(metrics)
             if did_outer and a.checkpoint_dir and a.checkpoint_every and \
                     (real_step // a.inner_steps) % a.checkpoint_every == 0:

@@ -225,3 +225,64 @@ def test_outer_nesterov_matches_torch_sgd(comm):
     ops.outer_nesterov(master, s2, delta, mom, None, 1.0, 0.7, 0.9, True)
     assert (master - p.detach()).abs().max().item() < 1e-6
     assert torch.equal(master, s2)
+
+
+# ----------------------------------------------------------------------------------- wgrad GEMM
+@pytest.mark.parametrize("M,N,K", [(3072, 1024, 4096), (1024, 1024, 32768), (1000, 264, 777), (32000, 1024, 2048),
+                                   (128, 512, 64)])
+def test_wgrad_gemm(M, N, K):
+    from nanodiloco_amd.ops.gemm import wgrad
+    dy = torch.randn(K, M, device=DEV).bfloat16()
+    x = torch.randn(K, N, device=DEV).bfloat16()
+    gw0 = torch.randn(M, N, device=DEV)
+    gw = gw0.clone()
+    wgrad(gw, dy, x)
+    ref_ = gw0 + dy.float().t() @ x.float()
+    assert rel(gw, ref_) < 1e-5, rel(gw, ref_)
+    gw2 = gw0.clone()
+    wgrad(gw2, dy, x)
+    assert torch.equal(gw, gw2)  # deterministic (no atomics)
+
+
+def test_wgrad_strided_views():
+    """Operands that are column slices of a wider buffer (fused q|k|v grads)."""
+    from nanodiloco_amd.ops.gemm import wgrad
+    K = 512
+    big = torch.randn(K, 384, device=DEV).bfloat16()
+    dy = big[:, 128:256]
+    x = torch.randn(K, 256, device=DEV).bfloat16()
+    gw = torch.zeros(128, 256, device=DEV)
+    wgrad(gw, dy, x)
+    assert rel(gw, dy.float().t() @ x.float()) < 1e-5
+
+
+# ----------------------------------------------------------------------------------- attention rope modes
+@pytest.mark.parametrize("hd,T", [(64, 200), (32, 130), (128, 96)])
+def test_attention_raw_qkv_rope_mode1(hd, T):
+    """Kernels applying RoPE on load (rope_mode 1 / fwd tables) on the raw projection output."""
+    from nanodiloco_amd.ops import _ext
+    from nanodiloco_amd.ops.attention import rope_cache
+    B, nh, nkv = 2, 4, 2
+    ld = (nh + 2 * nkv) * hd
+    qkv = torch.randn(B * T, ld, device=DEV).bfloat16()
+    cos, sin = rope_cache(T, hd, 10000.0, None, DEV)
+    L = _ext.lib()
+    s = _ext.stream_ptr(qkv.device)
+    k, v = qkv[:, nh * hd:], qkv[:, (nh + nkv) * hd:]
+    o = torch.empty(B * T, nh * hd, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, nh, T, device=DEV)
+    _ext.check(L.nd_attn_fwd(qkv.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(), B, nh, nkv, T,
+                             hd, ld, nh * hd, cos.data_ptr(), sin.data_ptr(), hd ** -0.5, s), "fwd")
+    xr = qkv.float().requires_grad_(True)
+    orf = _attn_ref(xr, cos, sin, B, T, nh, nkv, hd)
+    assert rel(o, orf) < 1e-2
+    do = torch.randn_like(orf).bfloat16()
+    orf.backward(do.float())
+    delta = torch.empty(B, nh, T, device=DEV)
+    _ext.check(L.nd_attn_bwd_pre(o.data_ptr(), do.data_ptr(), delta.data_ptr(), B, nh, T, hd, nh * hd, s), "pre")
+    dqkv = torch.empty_like(qkv)
+    dk, dv = dqkv[:, nh * hd:], dqkv[:, (nh + nkv) * hd:]
+    _ext.check(L.nd_attn_bwd(qkv.data_ptr(), k.data_ptr(), v.data_ptr(), do.data_ptr(), lse.data_ptr(),
+                             delta.data_ptr(), dqkv.data_ptr(), dk.data_ptr(), dv.data_ptr(), 0, B, nh, nkv, T, hd, ld,
+                             nh * hd, cos.data_ptr(), sin.data_ptr(), hd ** -0.5, 1, s), "bwd")
+    assert rel(dqkv, xr.grad) < 3e-2
