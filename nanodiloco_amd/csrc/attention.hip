@@ -195,6 +195,10 @@ __device__ __forceinline__ void load_tile(S& st, const bf16_t* base, int64_t str
 
 constexpr float LOG2E = 1.4426950408889634f;
 
+// Raw v_exp_f32 (no denormal range fix-up: exp2f lowers to ~6 extra VALU ops per call).  Inputs
+// here are <= 0 (scores minus a running max / LSE); results below 2^-126 flush to 0, harmless for P.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // Store a [HD x 32] transposed accumulator (rows = head dim in registers, col = row index on the
 // lane) as 8-B packed bf16 groups into row `out_row`.  With tables, the inverse RoPE rotation is
 // applied first: head-dim rows d and d + HD/2 sit in the same lane (o <-> o + NO/2, or register
@@ -257,8 +261,8 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_fwd_kernel(cons
                                                           int64_t ld, int64_t ldo, float scale,
                                                           const float* __restrict__ cosT, const float* __restrict__ sinT) {
   constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[BN * HD];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[BN * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * BN * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * BN * HD];
 
   const int nqb = (T + 127) / 128, bh_count = B * nh;
   const int qb = nqb - 1 - (int)(blockIdx.x / bh_count);  // longest causal rows first
@@ -284,65 +288,79 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_fwd_kernel(cons
   const int ntiles = (min(T, qb * 128 + 128) + BN - 1) / BN;
   typename std::conditional<ROPE, StageRope<BN, HD>, Stage<BN, HD>>::type sk;
   Stage<BN, HD> sv;
+  // double-buffered tiles: compute(buf j&1) | regs hold tile j+1 | store -> buf (j+1)&1 | ONE barrier
   load_tile<ROPE>(sk, Kb, ld, 0, T, cosT, sinT);
   sv.load(Vb, ld, 0, T);
+  sk.store(Ks);
+  sv.store(Vs);
+  __syncthreads();
+  if (ntiles > 1) {
+    load_tile<ROPE>(sk, Kb, ld, BN, T, cosT, sinT);
+    sv.load(Vb, ld, BN, T);
+  }
   for (int j = 0; j < ntiles; ++j) {
     const int k0 = j * BN;
-    __syncthreads();
-    sk.store(Ks);
-    sv.store(Vs);
-    __syncthreads();
-    if (j + 1 < ntiles) {  // prefetch the next tile; its latency hides under this tile's MFMAs
-      load_tile<ROPE>(sk, Kb, ld, k0 + BN, T, cosT, sinT);
-      sv.load(Vb, ld, k0 + BN, T);
-    }
-    if (k0 > q0w + 31) continue;  // whole tile above this wave's diagonal (wave-uniform)
-
-    f32x16 s[2];
+    const bf16_t* Kt = Ks + (j & 1) * (BN * HD);
+    const bf16_t* Vt = Vs + (j & 1) * (BN * HD);
+    if (k0 <= q0w + 31) {  // else: whole tile above this wave's diagonal (wave-uniform)
+      f32x16 s[2];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      s[kt] = f32x16{};
+      for (int kt = 0; kt < 2; ++kt) {
+        s[kt] = f32x16{};
 #pragma unroll
-      for (int t = 0; t < NT; ++t) s[kt] = mfma32(row_frag<HD>(Ks, kt * 32 + c32, t, h), qf[t], s[kt]);
-    }
-    const bool need_mask = (k0 + BN - 1 > q0w) || (k0 + BN > T);
-    float mx = -INFINITY;
+        for (int t = 0; t < NT; ++t) s[kt] = mfma32(row_frag<HD>(Kt, kt * 32 + c32, t, h), qf[t], s[kt]);
+      }
+      if ((k0 + BN - 1 > q0w) || (k0 + BN > T)) {
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = s[kt][r] * c;
-        if (need_mask) {
-          const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (key > qi || key >= T) v = -INFINITY;
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (key > qi || key >= T) s[kt][r] = -INFINITY;
+          }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;  // raw-score max -> log2 domain (c > 0)
+      const float mnew = fmaxf(m, mx);
+      const float alpha = fexp2(m - mnew);
+      m = mnew;
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(fmaf(s[kt][r], c, -mnew));
+          s[kt][r] = p;
+          rs += p;
         }
-        s[kt][r] = v;
-        mx = fmaxf(mx, v);
+      l = l * alpha + rs;
+      if (__any(alpha != 1.f)) {
+#pragma unroll
+        for (int o = 0; o < NO; ++o) oacc[o] *= alpha;
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m, mx);
-    const float alpha = exp2f(m - mnew);
-    m = mnew;
-    float rs = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(s[kt][r] - mnew);
-        s[kt][r] = p;
-        rs += p;
-      }
-    l = l * alpha + rs;
+        for (int sidx = 0; sidx < 2; ++sidx) {
+          const bf16x8 pf = pack_frag(s[kt], sidx);
 #pragma unroll
-    for (int o = 0; o < NO; ++o) oacc[o] *= alpha;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int sidx = 0; sidx < 2; ++sidx) {
-        const bf16x8 pf = pack_frag(s[kt], sidx);
-#pragma unroll
-        for (int o = 0; o < NO; ++o) oacc[o] = mfma32(tr_frag<HD>(Vs, kt * 32 + 16 * sidx, o * 32, g, i16), pf, oacc[o]);
-      }
+          for (int o = 0; o < NO; ++o)
+            oacc[o] = mfma32(tr_frag<HD>(Vt, kt * 32 + 16 * sidx, o * 32, g, i16), pf, oacc[o]);
+        }
+    }
+    if (j + 1 < ntiles) {
+      sk.store(Ks + ((j + 1) & 1) * (BN * HD));
+      sv.store(Vs + ((j + 1) & 1) * (BN * HD));
+    }
+    __syncthreads();
+    if (j + 2 < ntiles) {
+      load_tile<ROPE>(sk, Kb, ld, k0 + 2 * BN, T, cosT, sinT);
+      sv.load(Vb, ld, k0 + 2 * BN, T);
+    }
   }
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
@@ -391,8 +409,8 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
                                                              int64_t ld, int64_t ldo, float scale,
                                                              const float* __restrict__ cosT, const float* __restrict__ sinT) {
   constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[BN * HD];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[BN * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * BN * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * BN * HD];
 
   const int nqb = (T + 127) / 128, bh_count = B * nh;
   const int qb = nqb - 1 - (int)(blockIdx.x / bh_count);
@@ -426,45 +444,60 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
   Stage<BN, HD> sv;
   load_tile<ROPE>(sk, Kb, ld, 0, T, cosT, sinT);
   sv.load(Vb, ld, 0, T);
+  sk.store(Ks);
+  sv.store(Vs);
+  __syncthreads();
+  if (ntiles > 1) {
+    load_tile<ROPE>(sk, Kb, ld, BN, T, cosT, sinT);
+    sv.load(Vb, ld, BN, T);
+  }
   for (int j = 0; j < ntiles; ++j) {
     const int k0 = j * BN;
-    __syncthreads();
-    sk.store(Ks);
-    sv.store(Vs);
-    __syncthreads();
+    const bf16_t* Kt = Ks + (j & 1) * (BN * HD);
+    const bf16_t* Vt = Vs + (j & 1) * (BN * HD);
+    if (k0 <= q0w + 31) {
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        s[kt] = f32x16{};
+        dp[kt] = f32x16{};
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          s[kt] = mfma32(row_frag<HD>(Kt, kt * 32 + c32, t, h), qf[t], s[kt]);
+          dp[kt] = mfma32(row_frag<HD>(Vt, kt * 32 + c32, t, h), dof[t], dp[kt]);
+        }
+      }
+      const bool diag = (k0 + BN - 1 > q0w) || (k0 + BN > T) || (qi >= T);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float p = fexp2(fmaf(s[kt][r], c, -lse));
+          if (diag) {
+            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (!(key <= qi && key < T && qi < T)) p = 0.f;
+          }
+          dp[kt][r] = p * (dp[kt][r] - dlt);
+        }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int sidx = 0; sidx < 2; ++sidx) {
+          const bf16x8 dsf = pack_frag(dp[kt], sidx);
+#pragma unroll
+          for (int o = 0; o < NO; ++o)
+            dq[o] = mfma32(tr_frag<HD>(Kt, kt * 32 + 16 * sidx, o * 32, g, i16), dsf, dq[o]);
+        }
+    }
     if (j + 1 < ntiles) {
-      load_tile<ROPE>(sk, Kb, ld, k0 + BN, T, cosT, sinT);
-      sv.load(Vb, ld, k0 + BN, T);
+      sk.store(Ks + ((j + 1) & 1) * (BN * HD));
+      sv.store(Vs + ((j + 1) & 1) * (BN * HD));
     }
-    if (k0 > q0w + 31) continue;
-    f32x16 s[2], dp[2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      s[kt] = f32x16{};
-      dp[kt] = f32x16{};
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        s[kt] = mfma32(row_frag<HD>(Ks, kt * 32 + c32, t, h), qf[t], s[kt]);
-        dp[kt] = mfma32(row_frag<HD>(Vs, kt * 32 + c32, t, h), dof[t], dp[kt]);
-      }
+    __syncthreads();
+    if (j + 2 < ntiles) {
+      load_tile<ROPE>(sk, Kb, ld, k0 + 2 * BN, T, cosT, sinT);
+      sv.load(Vb, ld, k0 + 2 * BN, T);
     }
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const bool ok = key <= qi && key < T && qi < T;
-        const float p = ok ? exp2f(s[kt][r] * c - lse) : 0.f;
-        dp[kt][r] = p * (dp[kt][r] - dlt);
-      }
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int sidx = 0; sidx < 2; ++sidx) {
-        const bf16x8 dsf = pack_frag(dp[kt], sidx);
-#pragma unroll
-        for (int o = 0; o < NO; ++o) dq[o] = mfma32(tr_frag<HD>(Ks, kt * 32 + 16 * sidx, o * 32, g, i16), dsf, dq[o]);
-      }
   }
   if (qi < T)
     store_T<HD>(dQ + ((int64_t)b * T + qi) * ld + (int64_t)head * HD, dq, scale, h, ROPE_OUT ? cosT : nullptr, sinT, qi);
@@ -482,10 +515,10 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
                                                                const float* __restrict__ cosT,
                                                                const float* __restrict__ sinT) {
   constexpr int BQ = 64, NT = HD / 16, NO = HD / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * HD];
-  __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * HD];
-  __shared__ __attribute__((aligned(16))) float lse_s[BQ];
-  __shared__ __attribute__((aligned(16))) float del_s[BQ];
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[2 * BQ * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[2 * BQ * HD];
+  __shared__ __attribute__((aligned(16))) float lse_s[2 * BQ];
+  __shared__ __attribute__((aligned(16))) float del_s[2 * BQ];
 
   const int nkb = (T + 127) / 128, bk_count = B * nkv, rep = nh / nkv;
   const int kb = (int)(blockIdx.x / bk_count);  // small kb = longest query range: dispatched first
@@ -528,18 +561,25 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
       del_n = qq < T ? DELTA[rs + qq] : 0.f;
     }
   };
+  auto commit = [&](int buf) {
+    sq.store(Qs + buf * (BQ * HD));
+    sd.store(dOs + buf * (BQ * HD));
+    if (threadIdx.x < BQ) {
+      lse_s[buf * BQ + threadIdx.x] = lse_n;
+      del_s[buf * BQ + threadIdx.x] = del_n;
+    }
+  };
   prefetch(0);
+  commit(0);
+  __syncthreads();
+  if (nit > 1) prefetch(1);
   for (int it = 0; it < nit; ++it) {
     const int q0 = qstart + (it % ntq) * BQ;
-    __syncthreads();
-    sq.store(Qs);
-    sd.store(dOs);
-    if (threadIdx.x < BQ) {
-      lse_s[threadIdx.x] = lse_n;
-      del_s[threadIdx.x] = del_n;
-    }
-    __syncthreads();
-    if (it + 1 < nit) prefetch(it + 1);
+    const int buf = it & 1;
+    const bf16_t* Qt = Qs + buf * (BQ * HD);
+    const bf16_t* dOt = dOs + buf * (BQ * HD);
+    const float* lt = lse_s + buf * BQ;
+    const float* dt = del_s + buf * BQ;
 #pragma unroll
     for (int qs = 0; qs < BQ / 32; ++qs) {
       const int qsub = q0 + qs * 32;
@@ -548,19 +588,22 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qr = qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        s[r] = -lse_s[qr];
-        dp[r] = -del_s[qr];
+        s[r] = -lt[qr];
+        dp[r] = -dt[qr];
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        s = mfma32(row_frag<HD>(Qs, qs * 32 + c32, t, h), kf[t], s);
-        dp = mfma32(row_frag<HD>(dOs, qs * 32 + c32, t, h), vf[t], dp);
+        s = mfma32(row_frag<HD>(Qt, qs * 32 + c32, t, h), kf[t], s);
+        dp = mfma32(row_frag<HD>(dOt, qs * 32 + c32, t, h), vf[t], dp);
       }
+      const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int qq = qsub + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const bool ok = key <= qq && qq < T && key < T;
-        const float p = ok ? exp2f(s[r] * c) : 0.f;
+        float p = fexp2(s[r] * c);
+        if (diag) {
+          const int qq = qsub + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (!(key <= qq && qq < T && key < T)) p = 0.f;
+        }
         s[r] = p;
         dp[r] = p * dp[r];
       }
@@ -570,11 +613,14 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
         const bf16x8 dsf = pack_frag(dp, sidx);
 #pragma unroll
         for (int o = 0; o < NO; ++o) {
-          dv[o] = mfma32(tr_frag<HD>(dOs, qs * 32 + 16 * sidx, o * 32, g, i16), pf, dv[o]);
-          dk[o] = mfma32(tr_frag<HD>(Qs, qs * 32 + 16 * sidx, o * 32, g, i16), dsf, dk[o]);
+          dv[o] = mfma32(tr_frag<HD>(dOt, qs * 32 + 16 * sidx, o * 32, g, i16), pf, dv[o]);
+          dk[o] = mfma32(tr_frag<HD>(Qt, qs * 32 + 16 * sidx, o * 32, g, i16), dsf, dk[o]);
         }
       }
     }
+    if (it + 1 < nit) commit((it + 1) & 1);
+    __syncthreads();
+    if (it + 2 < nit) prefetch(it + 2);
   }
   if (key < T) {
     store_T<HD>(dK + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dk, scale, h, ROPE_OUT ? cosT : nullptr, sinT, key);

@@ -4,13 +4,14 @@
   nanodiloco_amd/_lib/libnd_runtime.so   csrc/runtime/*.cpp (host C++: token loader), g++ -O3
 
 Usage:  python -m nanodiloco_amd.csrc.build [--force] [--jobs N] [--save-temps]
-Incremental: an object is rebuilt only when its source or a header is newer.
+Incremental: an object is rebuilt only when the content hash of its source / headers / flags changed.
 """
 from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -30,11 +31,26 @@ def _hipcc() -> str:
     raise FileNotFoundError("hipcc not found (ROCm >= 7 required)")
 
 
-def _newer(src_files, target) -> bool:
-    if not os.path.exists(target):
+def _digest(files, extra="") -> str:
+    h = hashlib.sha256(extra.encode())
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def _stale(src_files, target, extra="") -> bool:
+    """Content-hash staleness (mtimes do not survive snapshot copies to the GPU box)."""
+    stamp = target + ".sha256"
+    if not os.path.exists(target) or not os.path.exists(stamp):
         return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(s) > t for s in src_files)
+    with open(stamp) as f:
+        return f.read().strip() != _digest(src_files, extra)
+
+
+def _mark(src_files, target, extra=""):
+    with open(target + ".sha256", "w") as f:
+        f.write(_digest(src_files, extra))
 
 
 def _run(cmd):
@@ -57,7 +73,7 @@ def build(force: bool = False, jobs: int = 0, save_temps: bool = False, verbose:
     for s in sources:
         o = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _newer([s] + headers, o):
+        if force or _stale([s] + sorted(headers), o, " ".join(flags)):
             todo.append((s, o))
     jobs = jobs or min(8, os.cpu_count() or 4)
 
@@ -67,6 +83,7 @@ def build(force: bool = False, jobs: int = 0, save_temps: bool = False, verbose:
         r = subprocess.run([hipcc] + flags + ["-c", s, "-o", o], capture_output=True, text=True, cwd=cwd)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed on {os.path.basename(s)}:\n{r.stderr[-6000:]}")
+        _mark([s] + sorted(headers), o, " ".join(flags))
         return s
 
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
@@ -74,16 +91,18 @@ def build(force: bool = False, jobs: int = 0, save_temps: bool = False, verbose:
             if verbose:
                 print(f"[build] compiled {os.path.basename(s)}", flush=True)
     kern = os.path.join(LIB_DIR, "libnd_kernels.so")
-    if force or todo or _newer(objs, kern):
+    if force or todo or _stale(objs, kern):
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", kern + ".tmp"] + objs)
         os.replace(kern + ".tmp", kern)
+        _mark(objs, kern)
     # host runtime (plain C++)
     rt_src = sorted(glob.glob(os.path.join(HERE, "runtime", "*.cpp")))
     rt = os.path.join(LIB_DIR, "libnd_runtime.so")
-    if rt_src and (force or _newer(rt_src, rt)):
+    if rt_src and (force or _stale(rt_src, rt)):
         cxx = shutil.which("g++") or shutil.which("c++")
         _run([cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", "-o", rt + ".tmp"] + rt_src)
         os.replace(rt + ".tmp", rt)
+        _mark(rt_src, rt)
     return {"kernels": kern, "runtime": rt, "compiled": [os.path.basename(s) for s, _ in todo]}
 
 

@@ -16,6 +16,7 @@
 //   * XCD-aware block remap so the workgroups sharing an A row-panel run on one XCD's L2.
 // Tile: 128 x 128 per 256-thread workgroup (2 x 2 waves of 64 x 64, 2 x 2 v_mfma_f32_32x32x16_bf16).
 #include "common.h"
+#include <cstdlib>
 
 using namespace nd;
 
@@ -197,8 +198,7 @@ __global__ void __launch_bounds__(512, 2) wgrad256_kernel(const bf16_t* __restri
                                                           int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
                                                           int kchunk) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  bf16_t* As[2] = {smem, smem + BK2 * BM2};
-  bf16_t* Bs[2] = {smem + 2 * BK2 * BM2, smem + 2 * BK2 * BM2 + BK2 * BN2};
+  // buffer b: A at smem + b * BK2 * BM2, B at smem + 2 * BK2 * BM2 + b * BK2 * BN2
   const int tn_count = (N + BN2 - 1) / BN2;
   const int tiles = ((M + BM2 - 1) / BM2) * tn_count;
   const int id = xcd_remap(blockIdx.x, tiles * S);
@@ -220,8 +220,8 @@ __global__ void __launch_bounds__(512, 2) wgrad256_kernel(const bf16_t* __restri
   if (nk > 0) {
     la.load(A, lda, kbeg, kend, m0, M);
     lb.load(B, ldb, kbeg, kend, n0, N);
-    la.store(As[0]);
-    lb.store(Bs[0]);
+    la.store(smem);
+    lb.store(smem + 2 * BK2 * BM2);
   }
   __syncthreads();
   if (nk > 1) {
@@ -229,8 +229,8 @@ __global__ void __launch_bounds__(512, 2) wgrad256_kernel(const bf16_t* __restri
     lb.load(B, ldb, kbeg + BK2, kend, n0, N);
   }
   for (int kt = 0; kt < nk; ++kt) {
-    const bf16_t* a_t = As[kt & 1];
-    const bf16_t* b_t = Bs[kt & 1];
+    const bf16_t* a_t = smem + (kt & 1) * BK2 * BM2;
+    const bf16_t* b_t = smem + 2 * BK2 * BM2 + (kt & 1) * BK2 * BN2;
 #pragma unroll
     for (int ks = 0; ks < BK2 / 16; ++ks) {
       bf16x8 fb[2];
@@ -244,14 +244,160 @@ __global__ void __launch_bounds__(512, 2) wgrad256_kernel(const bf16_t* __restri
       }
     }
     if (kt + 1 < nk) {
-      la.store(As[(kt + 1) & 1]);
-      lb.store(Bs[(kt + 1) & 1]);
+      la.store(smem + ((kt + 1) & 1) * BK2 * BM2);
+      lb.store(smem + 2 * BK2 * BM2 + ((kt + 1) & 1) * BK2 * BN2);
     }
     __syncthreads();
     if (kt + 2 < nk) {
       la.load(A, lda, kbeg + (kt + 2) * BK2, kend, m0, M);
       lb.load(B, ldb, kbeg + (kt + 2) * BK2, kend, n0, N);
     }
+  }
+  float* out = S == 1 ? C : slab + (int64_t)split * M * N;
+  const int64_t ldo = S == 1 ? ldc : N;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int n = n0 + wn * 64 + b * 32 + c32;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M) {
+          float* p = out + (int64_t)m * ldo + n;
+          if (S == 1) *p += acc[a][b][r];
+          else *p = acc[a][b][r];
+        }
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA variant (the production path): same 256 x 256 / 8-wave / 128 x 64-per-wave geometry, but
+// tiles move global -> LDS with global_load_lds_dwordx4 (no VGPR round trip, no ds_write issue cost,
+// which bounded the register-staged kernel).  The LDS image is lane-linear per wave-instruction
+// (1 KiB = two 512-B rows), so the bank swizzle is applied on the SOURCE address: the lane that
+// lands in physical chunk p of row r loads logical chunk p ^ ((r & 3) << 2), and the transposing
+// reads use the same involution.  BK = 64, two buffers (128 KiB LDS, one workgroup per CU):
+//   barrier | DMA tile k+1 -> buf[(k+1)&1] | 32 MFMAs per wave on buf[k&1] | vmcnt(0)+barrier
+// A K-tail tile (rows past kend must read as zero) falls back to register staging with zero fill.
+namespace {
+constexpr int BK3 = 64;
+typedef __attribute__((address_space(3))) void lds_void;
+
+// One 16-B-per-lane LDS-DMA wave-instruction, issued from inline asm so hipcc does not track it:
+// otherwise it conservatively waits vmcnt(0) before the first LDS read of the OTHER buffer, which
+// serialises the DMA of tile k+1 with the MFMAs of tile k.  The caller owns the vmcnt wait.
+// M0 (DMA destination base) is compiler-reserved: saved/restored inside the same statement.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_byte_addr)
+      : "memory");
+}
+
+__device__ __forceinline__ void dma_tile(bf16_t* tile, const bf16_t* base, int64_t ld, int k0, int c0, int cols) {
+  // 64 rows x 512 B = 32 wave-instructions of 1 KiB; wave w issues rows (2i, 2i+1) for i = w, w+8, w+16, w+24
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t tile_addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)tile);
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int pair = w + 8 * it;
+    const int row = 2 * pair + (lane >> 5);
+    const int p = lane & 31;                       // physical chunk written by this lane
+    const int c = p ^ ((row & 3) << 2);            // logical chunk it must carry
+    int col = c0 + c * 8;
+    col = col < cols ? col : cols - 8;             // clamp: tail columns only feed masked outputs
+    const bf16_t* src = base + (int64_t)(k0 + row) * ld + col;
+    glds16(src, __builtin_amdgcn_readfirstlane(tile_addr + pair * 1024));
+  }
+}
+
+__device__ __forceinline__ void reg_tile(bf16_t* tile, const bf16_t* base, int64_t ld, int k0, int kend, int c0,
+                                         int cols) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int c = threadIdx.x + it * 512;
+    const int row = c >> 5, ch = c & 31;
+    const int k = k0 + row, col = c0 + ch * 8;
+    bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (k < kend && col < cols) v = *reinterpret_cast<const bf16x8*>(base + (int64_t)k * ld + col);
+    *reinterpret_cast<bf16x8*>(&tile[toff2(row, ch * 8)]) = v;
+  }
+}
+}  // namespace
+
+__global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                           float* __restrict__ C, float* __restrict__ slab, int M,
+                                                           int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
+                                                           int kchunk) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  constexpr int TA = BK3 * BM2, TB = BK3 * BN2;  // elements per operand tile
+  const int tn_count = (N + BN2 - 1) / BN2;
+  const int tiles = ((M + BM2 - 1) / BM2) * tn_count;
+  const int id = xcd_remap(blockIdx.x, tiles * S);
+  const int tile = id / S, split = id % S;
+  const int m0 = (tile / tn_count) * BM2, n0 = (tile % tn_count) * BN2;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int wm = w >> 2, wn = w & 3;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+
+  const int nk = kend > kbeg ? (kend - kbeg + BK3 - 1) / BK3 : 0;
+  auto stage = [&](int kt) {
+    bf16_t* ta = smem + (kt & 1) * (TA + TB);
+    bf16_t* tb = ta + TA;
+    const int k0 = kbeg + kt * BK3;
+    if (k0 + BK3 <= kend) {
+      dma_tile(ta, A, lda, k0, m0, M);
+      dma_tile(tb, B, ldb, k0, n0, N);
+    } else {
+      reg_tile(ta, A, lda, k0, kend, m0, M);
+      reg_tile(tb, B, ldb, k0, kend, n0, N);
+    }
+  };
+  if (nk > 0) stage(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) stage(kt + 1);
+    const bf16_t* a_t = smem + (kt & 1) * (TA + TB);
+    const bf16_t* b_t = a_t + TA;
+    // fragments of k-step ks+1 are read while the 8 MFMAs of k-step ks run (register double buffer)
+    bf16x8 fa[2][4], fb[2][2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) fb[0][b] = frag2(b_t, 0, wn * 64 + b * 32, g, i16);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) fa[0][a] = frag2(a_t, 0, wm * 128 + a * 32, g, i16);
+#pragma unroll
+    for (int ks = 0; ks < BK3 / 16; ++ks) {
+      const int cur = ks & 1, nxt = cur ^ 1;
+      if (ks + 1 < BK3 / 16) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) fb[nxt][b] = frag2(b_t, (ks + 1) * 16, wn * 64 + b * 32, g, i16);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) fa[nxt][a] = frag2(a_t, (ks + 1) * 16, wm * 128 + a * 32, g, i16);
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(fa[cur][a], fb[cur][b], acc[a][b]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile kt+1 has landed
+    __syncthreads();                                  // ... everyone's, and buf[kt&1] is free again
   }
   float* out = S == 1 ? C : slab + (int64_t)split * M * N;
   const int64_t ldo = S == 1 ? ldc : N;
@@ -328,7 +474,18 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
   int S;
   const int large = plan(M, N, K, &S);
   if (S > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
-  if (large) {
+  const char* ev = getenv("ND_WGRAD_VARIANT");  // "reg": register-staged 256 kernel (for A/B runs)
+  const int variant = (ev && ev[0] == 'r') ? 1 : 0;
+  if (large && variant == 0 && M >= 8 && N >= 8) {
+    const int kchunk = ((K + S - 1) / S + BK3 - 1) / BK3 * BK3;
+    const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
+    const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB
+    static const hipError_t attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_dma_kernel),
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)attr_ok;
+    hipLaunchKernelGGL(wgrad_dma_kernel, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B, C,
+                       slab, M, N, K, lda, ldb, ldc, S, kchunk);
+  } else if (large) {
     const int kchunk = ((K + S - 1) / S + BK2 - 1) / BK2 * BK2;
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK2 * (BM2 + BN2) * sizeof(bf16_t);
