@@ -64,11 +64,25 @@ __device__ __forceinline__ bf16x8 load16(const bf16_t* p) { return *reinterpret_
 __device__ __forceinline__ bf16x8 zero8() { return bf16x8{0, 0, 0, 0, 0, 0, 0, 0}; }
 
 // Element offset of (row, col) inside an XOR-swizzled [rows][HD] bf16 LDS tile (16-B chunks).
+// The XOR key s(row) must keep BOTH access kinds conflict-free:
+//  * row reads (ds_read_b128): 16 consecutive rows at one logical chunk -> 16 distinct bank slots;
+//  * transposed reads (ds_read_b64_tr_b16): a 32-lane half reads rows r0..r0+3 (r0 % 4 == 0), 64 B
+//    each, so rows that share a bank row must differ in the chunk bit that picks the 64-B half.
+// HD=64 (two 128-B rows per 256-B bank row): s = bitreverse3((row >> 1) & 7)  [rows r0, r0+2 differ in bit 2]
+// HD=128 (one row per bank row):             s = ((row & 3) << 2) | ((row >> 2) & 3)
+// HD=32 (four 64-B rows per bank row):        s = (row >> 2) & 3
 template <int HD>
 __device__ __forceinline__ int soff(int row, int col) {
-  constexpr int CPR = HD / 8;                          // 16-B chunks per row
-  constexpr int RPB = (16 / CPR) > 0 ? 16 / CPR : 1;   // rows per 256-B bank row
-  const int ch = (col >> 3) ^ ((row / RPB) & (CPR - 1));
+  int key;
+  if constexpr (HD == 64) {
+    const int u = (row >> 1) & 7;
+    key = ((u & 1) << 2) | (u & 2) | ((u >> 2) & 1);
+  } else if constexpr (HD == 128) {
+    key = ((row & 3) << 2) | ((row >> 2) & 3);
+  } else {
+    key = (row >> 2) & 3;
+  }
+  const int ch = (col >> 3) ^ key;
   return row * HD + ch * 8 + (col & 7);
 }
 

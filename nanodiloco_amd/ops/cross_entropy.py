@@ -47,6 +47,9 @@ class LMHeadCEFn(torch.autograd.Function):
         loss_sum = torch.zeros(1, dtype=torch.float32, device=y.device)
         hip = _ext.use_hip(y)
         chunk = chunk_rows or _chunk_rows(V, y.element_size() if hip else 4)
+        if not chunk_rows and n > chunk:  # equal-sized chunks: one GEMM shape, one tuned kernel
+            nch = -(-n // chunk)
+            chunk = (-(-n // nch) + 255) // 256 * 256
         for s in range(0, n, chunk):
             e = min(n, s + chunk)
             yc, tc = y[s:e], targets[s:e]
