@@ -18,6 +18,7 @@
 #include "common.h"
 #include <cstdlib>
 
+
 using namespace nd;
 
 typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
@@ -334,6 +335,7 @@ __device__ __forceinline__ void reg_tile(bf16_t* tile, const bf16_t* base, int64
 }
 }  // namespace
 
+template <bool SCHED>
 __global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                            float* __restrict__ C, float* __restrict__ slab, int M,
                                                            int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
@@ -395,6 +397,15 @@ __global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restr
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(fa[cur][a], fb[cur][b], acc[a][b]);
+      if (SCHED && ks + 1 < BK3 / 16) {
+        // interleave the 12 transposing reads of k-step ks+1 between the 8 MFMAs of k-step ks
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // 2 DS reads
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile kt+1 has landed
     __syncthreads();                                  // ... everyone's, and buf[kt&1] is free again
@@ -474,17 +485,27 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
   int S;
   const int large = plan(M, N, K, &S);
   if (S > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
-  const char* ev = getenv("ND_WGRAD_VARIANT");  // "reg": register-staged 256 kernel (for A/B runs)
+  // ND_WGRAD_VARIANT (A/B runs): "reg" register-staged 256 kernel, "dma0" LDS-DMA without the
+  // sched_group_barrier interleave; default: LDS-DMA with the interleave.
+  const char* ev = getenv("ND_WGRAD_VARIANT");
   const int variant = (ev && ev[0] == 'r') ? 1 : 0;
+  const bool sched = !(ev && ev[0] == 'd' && ev[3] == '0');
   if (large && variant == 0 && M >= 8 && N >= 8) {
     const int kchunk = ((K + S - 1) / S + BK3 - 1) / BK3 * BK3;
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB
-    static const hipError_t attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_dma_kernel),
-                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    static const hipError_t attr_ok =
+        (hipError_t)(hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_dma_kernel<true>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) |
+                     hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_dma_kernel<false>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     (void)attr_ok;
-    hipLaunchKernelGGL(wgrad_dma_kernel, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B, C,
-                       slab, M, N, K, lda, ldb, ldc, S, kchunk);
+    if (sched)
+      hipLaunchKernelGGL(wgrad_dma_kernel<true>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A,
+                         (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
+    else
+      hipLaunchKernelGGL(wgrad_dma_kernel<false>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A,
+                         (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
   } else if (large) {
     const int kchunk = ((K + S - 1) / S + BK2 - 1) / BK2 * BK2;
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);

@@ -38,7 +38,8 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
                                                     float* __restrict__ m, float* __restrict__ v, void* __restrict__ sh,
                                                     int64_t n, const float* __restrict__ part, int nparts, float lr,
                                                     float b1, float b2, float eps, float wd, float bc1, float bc2,
-                                                    float max_norm, float* __restrict__ norm_out) {
+                                                    float max_norm, float* __restrict__ norm_out, int skip_nonfinite,
+                                                    int* __restrict__ skipped) {
   __shared__ float red[4];
   float coef = 1.f;
   if (part) {
@@ -48,6 +49,12 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
     const float norm = sqrtf(t);
     if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
     if (norm_out && blockIdx.x == 0 && threadIdx.x == 0) norm_out[0] = norm;
+    // device-side guard: every block sees the same norm, so a NaN/Inf step is skipped everywhere
+    // (no host sync); the step counter on the host still advances, like torch's GradScaler skip.
+    if (skip_nonfinite && !isfinite(norm)) {
+      if (skipped && blockIdx.x == 0 && threadIdx.x == 0) skipped[0] += 1;
+      return;
+    }
   }
   const float decay = 1.f - lr * wd;
   const float step = lr / bc1;
@@ -87,14 +94,14 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
 
 ND_API int nd_adamw_step(float* p, const float* g, float* m, float* v, void* sh, int shdt, int64_t n,
                          const float* part, int nparts, float lr, float b1, float b2, float eps, float wd, float bc1,
-                         float bc2, float max_norm, float* norm_out, hipStream_t s) {
+                         float bc2, float max_norm, float* norm_out, int skip_nonfinite, int* skipped, hipStream_t s) {
   const unsigned grid = stream_grid(n >> 2);
   if (sh && shdt == BF16)
     hipLaunchKernelGGL(adamw_kernel<BF16>, dim3(grid), dim3(256), 0, s, p, g, m, v, sh, n, part, nparts, lr, b1, b2, eps,
-                       wd, bc1, bc2, max_norm, norm_out);
+                       wd, bc1, bc2, max_norm, norm_out, skip_nonfinite, skipped);
   else
     hipLaunchKernelGGL(adamw_kernel<F32>, dim3(grid), dim3(256), 0, s, p, g, m, v, nullptr, n, part, nparts, lr, b1, b2,
-                       eps, wd, bc1, bc2, max_norm, norm_out);
+                       eps, wd, bc1, bc2, max_norm, norm_out, skip_nonfinite, skipped);
   ND_LAUNCH_CHECK();
 }
 

@@ -120,7 +120,7 @@ def _declare(L: ctypes.CDLL):
         "nd_embedding_bwd": [P, P, P, L64, I, I, P],
         # optimizer / outer step (flat buffers)
         "nd_sumsq_partial": [P, L64, P, I, P],
-        "nd_adamw_step": [P, P, P, P, P, I, L64, P, I, F, F, F, F, F, F, F, F, P, P],
+        "nd_adamw_step": [P, P, P, P, P, I, L64, P, I, F, F, F, F, F, F, F, F, P, I, P, P],
         "nd_pseudograd": [P, P, P, I, L64, P],
         "nd_outer_nesterov": [P, P, P, I, P, P, I, L64, F, F, F, I, P, P, P],
         "nd_axpby": [P, P, L64, F, F, P],

@@ -43,11 +43,14 @@ def global_grad_norm(grad: torch.Tensor) -> torch.Tensor:
 def adamw_step(master: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
                shadow: Optional[torch.Tensor], step: int, lr: float, betas=(0.9, 0.999), eps: float = 1e-8,
                weight_decay: float = 0.01, max_norm: Optional[float] = 1.0,
-               norm_out: Optional[torch.Tensor] = None) -> None:
+               norm_out: Optional[torch.Tensor] = None, skip_nonfinite: bool = False,
+               skipped: Optional[torch.Tensor] = None) -> None:
     """Clip-by-global-norm + AdamW (torch.optim.AdamW semantics) over flat fp32 buffers.
 
     ``step`` is the 1-based AdamW step count (bias correction).  If ``norm_out`` is given, the
     pre-clip global grad norm is written to it (device scalar, for logging without a sync).
+    ``skip_nonfinite``: if the global grad norm is NaN/Inf the update is skipped on the device (no
+    host sync) and ``skipped`` (int32 device scalar) is incremented.
     """
     b1, b2 = betas
     bc1 = 1.0 - b1 ** step
@@ -57,22 +60,28 @@ def adamw_step(master: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, 
         part = torch.empty(SUMSQ_BLOCKS, dtype=torch.float32, device=master.device)
         L = _ext.lib()
         s = _ext.stream_ptr(master.device)
-        if max_norm is not None or norm_out is not None:
+        need_norm = max_norm is not None or norm_out is not None or skip_nonfinite
+        if need_norm:
             _ext.check(L.nd_sumsq_partial(_ext.ptr(grad), n, _ext.ptr(part), SUMSQ_BLOCKS, s), "nd_sumsq_partial")
         sh = shadow if (shadow is not None and shadow.data_ptr() != master.data_ptr()) else None
         _ext.check(L.nd_adamw_step(_ext.ptr(master), _ext.ptr(grad), _ext.ptr(exp_avg), _ext.ptr(exp_avg_sq),
                                    _ext.ptr(sh), _ext.dtcode(sh) if sh is not None else 0, n,
-                                   _ext.ptr(part) if (max_norm is not None or norm_out is not None) else 0,
+                                   _ext.ptr(part) if need_norm else 0,
                                    SUMSQ_BLOCKS, float(lr), float(b1), float(b2), float(eps), float(weight_decay),
                                    float(bc1), float(bc2), float(max_norm if max_norm is not None else -1.0),
-                                   _ext.ptr(norm_out), s), "nd_adamw_step")
+                                   _ext.ptr(norm_out), 1 if skip_nonfinite else 0, _ext.ptr(skipped), s),
+                   "nd_adamw_step")
         return
     # ---- torch reference (same op order as torch.optim.AdamW single-tensor path)
     g = grad
-    if max_norm is not None or norm_out is not None:
+    if max_norm is not None or norm_out is not None or skip_nonfinite:
         total = grad.norm()
         if norm_out is not None:
             norm_out.copy_(total.reshape(norm_out.shape))
+        if skip_nonfinite and not bool(torch.isfinite(total)):
+            if skipped is not None:
+                skipped += 1
+            return
         if max_norm is not None:
             coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
             g = grad * coef

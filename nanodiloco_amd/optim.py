@@ -21,7 +21,7 @@ from .models.param_store import ParamStore
 
 class FlatAdamW:
     def __init__(self, store: ParamStore, lr: float = 4e-4, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.01, max_grad_norm: Optional[float] = 1.0):
+                 weight_decay: float = 0.01, max_grad_norm: Optional[float] = 1.0, skip_nonfinite: bool = False):
         self.store = store
         self.lr = lr
         self.betas = tuple(betas)
@@ -32,6 +32,8 @@ class FlatAdamW:
         self.exp_avg_sq = store.new_flat()
         self.step_count = 0
         self.last_grad_norm = torch.zeros(1, dtype=torch.float32, device=store.device)
+        self.skip_nonfinite = skip_nonfinite
+        self.skipped_steps = torch.zeros(1, dtype=torch.int32, device=store.device)
         # torch-style param_groups so code reading `param_groups[0]["lr"]` keeps working
         self.param_groups = [{"lr": lr, "params": store.names}]
 
@@ -41,7 +43,8 @@ class FlatAdamW:
         self.step_count += 1
         ops.adamw_step(self.store.master, self.store.grad, self.exp_avg, self.exp_avg_sq, self.store.shadow,
                        self.step_count, lr, self.betas, self.eps, self.weight_decay, self.max_grad_norm,
-                       norm_out=self.last_grad_norm)
+                       norm_out=self.last_grad_norm, skip_nonfinite=self.skip_nonfinite,
+                       skipped=self.skipped_steps)
 
     def zero_grad(self, set_to_none: bool = False):
         self.store.zero_grad()

@@ -74,6 +74,10 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
                   num_workers=world // inner_dp)
     if world == 1:
         return env
+    # failure detection: a hung / failed collective surfaces as an error on every rank (instead of a
+    # silent hang) after `timeout_s`; torchrun --max-restarts + --resume then restart from the last
+    # outer-step checkpoint.
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if not dist.is_initialized():
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":

@@ -74,6 +74,8 @@ class TrainArgs:
     tokenizer: str = "huggyllama/llama-7b"
     debug_checks: bool = False
     mask_pad_labels: bool = True
+    skip_nonfinite: bool = False   # device-side skip of inner steps whose grad norm is NaN/Inf (no host sync)
+    collective_timeout_s: float = 1800.0
     phase_timing: bool = True      # HIP-event timing of fwd+bwd / inner optimizer / outer step (logged)
     profile_dir: Optional[str] = None   # torch.profiler Chrome trace of `profile_steps` steps
     profile_steps: int = 0
@@ -106,7 +108,8 @@ class Trainer:
         if a.total_steps % a.inner_steps:
             raise ValueError("total_steps must be a multiple of inner_steps")  # REF main.py:69
         ops.set_backend(a.ops)
-        self.env = env or init_distributed(a.backend, a.inner_dp, device=None if a.device == "auto" else a.device)
+        self.env = env or init_distributed(a.backend, a.inner_dp, device=None if a.device == "auto" else a.device,
+                                           timeout_s=a.collective_timeout_s)
         e = self.env
         self.llama_config: LlamaConfig = resolve_llama_config(a.llama_config_file)
         self.run_config = load_config_from_file(a.wandb_config_file) if a.wandb_config_file else default_run_config()
@@ -116,7 +119,8 @@ class Trainer:
         self.compute_dtype = _dtype(a.dtype, e.device)
         self.model = LlamaForCausalLM(self.llama_config, e.device, self.compute_dtype,
                                       activation_checkpointing=a.activation_checkpointing).init_weights(a.seed)
-        inner = FlatAdamW(self.model.store, lr=a.lr, weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm)
+        inner = FlatAdamW(self.model.store, lr=a.lr, weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm,
+                          skip_nonfinite=a.skip_nonfinite)
         outer = FlatOuterNesterov(self.model.store, lr=a.outer_lr, momentum=a.outer_momentum)
         self.diloco = Diloco(self.model, inner, outer, a.warmup_steps, a.total_steps, a.inner_steps, self.outer_steps,
                              env=e, comm_dtype=_dtype(a.comm_dtype, e.device), bucket_mb=a.bucket_mb,
@@ -200,6 +204,8 @@ class Trainer:
                     "grad_norm": float(self.diloco.inner_optimizer.last_grad_norm.item()),
                     "outer_step": self.diloco.outer_step_count,
                 }
+                if a.skip_nonfinite:
+                    metrics["skipped_steps"] = int(self.diloco.inner_optimizer.skipped_steps.item())
                 if did_outer:
                     metrics["bytes_outer"] = self.diloco.bytes_per_outer_step
                     metrics["sync_s"] = self.diloco.avg_sync_time

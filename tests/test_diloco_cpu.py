@@ -140,3 +140,19 @@ def test_single_process_no_group():
     st.master.sub_(2.0)
     dl.outer_step()  # W=1: avg delta = 2 -> -0.7*(2+1.8) = -2.66
     assert torch.allclose(st.master[: st.num_params], (base - 2.66)[: st.num_params], atol=1e-5)
+
+
+def test_skip_nonfinite_step():
+    from nanodiloco_amd.ops import adamw_step
+    n = 128
+    master = torch.randn(n)
+    before = master.clone()
+    m, v = torch.zeros(n), torch.zeros(n)
+    g = torch.randn(n)
+    g[3] = float("nan")
+    skipped = torch.zeros(1, dtype=torch.int32)
+    adamw_step(master, g, m, v, None, 1, 1e-3, skip_nonfinite=True, skipped=skipped)
+    assert torch.equal(master, before) and int(skipped.item()) == 1
+    g[3] = 0.0
+    adamw_step(master, g, m, v, None, 1, 1e-3, skip_nonfinite=True, skipped=skipped)
+    assert not torch.equal(master, before) and int(skipped.item()) == 1

@@ -286,3 +286,15 @@ def test_attention_raw_qkv_rope_mode1(hd, T):
                              delta.data_ptr(), dqkv.data_ptr(), dk.data_ptr(), dv.data_ptr(), 0, B, nh, nkv, T, hd, ld,
                              nh * hd, cos.data_ptr(), sin.data_ptr(), hd ** -0.5, 1, s), "bwd")
     assert rel(dqkv, xr.grad) < 3e-2
+
+
+def test_adamw_skip_nonfinite_on_device():
+    n = 4096
+    master = torch.randn(n, device=DEV)
+    before = master.clone()
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    g[100] = float("inf")
+    skipped = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ops.adamw_step(master, g, m, v, None, 1, 1e-3, skip_nonfinite=True, skipped=skipped)
+    assert torch.equal(master, before) and int(skipped.item()) == 1
