@@ -52,7 +52,7 @@ class _GradHook(torch.autograd.Function):
 
 class LlamaForCausalLM:
     def __init__(self, config: LlamaConfig, device="cpu", compute_dtype: torch.dtype = torch.float32,
-                 store: Optional[ParamStore] = None, activation_checkpointing: bool = False):
+                 store: Optional[ParamStore] = None, activation_checkpointing: bool = False, fp8: bool = False):
         self.config = config
         self.device = torch.device(device)
         self.compute_dtype = compute_dtype
@@ -68,6 +68,12 @@ class LlamaForCausalLM:
         self._gu_names = [g for g in groups[1::2]]
         self.layer_hook: Optional[Callable[[int], None]] = None
         self.training = True
+        self.fp8 = None
+        if fp8:
+            if compute_dtype != torch.bfloat16 or self.device.type != "cuda":
+                raise ValueError("fp8 needs bf16 compute on an MI355X")
+            from ..ops.fp8 import Fp8Linears
+            self.fp8 = Fp8Linears(self.device)
 
     # ------------------------------------------------------------------ init / io
     @torch.no_grad()
@@ -127,22 +133,28 @@ class LlamaForCausalLM:
         return self.store.fused_view(which, names)
 
     # ------------------------------------------------------------------ forward
+    def _linear(self, key, x, w, gw):
+        if self.fp8 is not None:
+            return self.fp8(key, x, w, gw, self.store.version)
+        return ops.linear(x, w, gw)
+
     def _layer(self, i, h, y, cos, sin, B, T, next_norm):
         c = self.config
         p = f"model.layers.{i}."
         cdt = self.compute_dtype
         eps = c.rms_norm_eps
         qn = self._qkv_names[i]
-        qkv = ops.linear(y, self._fused(qn, "shadow"), self._fused(qn, "grad"))
+        qkv = self._linear(f"{i}.qkv", y, self._fused(qn, "shadow"), self._fused(qn, "grad"))
         o = ops.attention(qkv, cos, sin, B, T, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
                           inplace=True)
-        a = ops.linear(o, self._w(p + "self_attn.o_proj.weight"), self._g(p + "self_attn.o_proj.weight"))
+        a = self._linear(f"{i}.o", o, self._w(p + "self_attn.o_proj.weight"), self._g(p + "self_attn.o_proj.weight"))
         y, h = ops.add_rmsnorm(h, a, self._m(p + "post_attention_layernorm.weight"),
                                self._g(p + "post_attention_layernorm.weight"), eps, cdt)
         gn = self._gu_names[i]
-        gu = ops.linear(y, self._fused(gn, "shadow"), self._fused(gn, "grad"))
+        gu = self._linear(f"{i}.gu", y, self._fused(gn, "shadow"), self._fused(gn, "grad"))
         act = ops.swiglu(gu)
-        m = ops.linear(act, self._w(p + "mlp.down_proj.weight"), self._g(p + "mlp.down_proj.weight"))
+        m = self._linear(f"{i}.down", act, self._w(p + "mlp.down_proj.weight"),
+                         self._g(p + "mlp.down_proj.weight"))
         return m, h
 
     def hidden_states(self, input_ids: torch.Tensor) -> torch.Tensor:

@@ -64,6 +64,7 @@ class ParamStore:
         else:
             self.shadow = torch.zeros(self.numel, dtype=compute_dtype, device=self.device)
         self._views: Dict[Tuple[str, str], torch.Tensor] = {}
+        self.version = 0  # bumped whenever the weights change (optimizer / outer step / load)
 
     # ------------------------------------------------------------------ views
     def range(self, name: str) -> Tuple[int, int]:
@@ -138,6 +139,7 @@ class ParamStore:
                         raise ValueError(f"shape mismatch for {n}: {tuple(t.shape)} vs {self.shapes[n]}")
                     self.master_view(n).copy_(t.to(torch.float32))
         self.sync_shadow()
+        self.version += 1
 
     def new_flat(self, dtype=torch.float32, device=None, pin: bool = False) -> torch.Tensor:
         dev = torch.device(device) if device is not None else self.device

@@ -124,6 +124,8 @@ def _declare(L: ctypes.CDLL):
         "nd_pseudograd": [P, P, P, I, L64, P],
         "nd_outer_nesterov": [P, P, P, I, P, P, I, L64, F, F, F, I, P, P, P],
         "nd_axpby": [P, P, L64, F, F, P],
+        # fp8 quantisation
+        "nd_fp8_cast": [P, I, L64, P, P, I, P, I, P],
         # weight-gradient GEMM
         "nd_wgrad_splits": [I, I, I],
         "nd_wgrad": [P, P, P, P, I, I, I, L64, L64, L64, P],

@@ -45,6 +45,7 @@ class FlatAdamW:
                        self.step_count, lr, self.betas, self.eps, self.weight_decay, self.max_grad_norm,
                        norm_out=self.last_grad_norm, skip_nonfinite=self.skip_nonfinite,
                        skipped=self.skipped_steps)
+        self.store.version += 1
 
     def zero_grad(self, set_to_none: bool = False):
         self.store.zero_grad()

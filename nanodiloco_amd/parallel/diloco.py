@@ -126,6 +126,8 @@ class Diloco:
         """clip(1.0) + AdamW at the scheduled lr, advance the schedule, zero grads."""
         lr = self.scheduler.lr()
         self.inner_optimizer.step(lr)
+        if getattr(self.model, "fp8", None) is not None:
+            self.model.fp8.recipe.update()  # fp8 delayed scaling: roll amax history once per inner step
         self.scheduler.step()
         self.store.zero_grad()
         self.local_step += 1
@@ -170,6 +172,7 @@ class Diloco:
                                sh_full[ga:gb] if sh_full is not None else None, inv_w, opt.lr, opt.momentum,
                                first, drift_base=self.drift_base[x:y] if self.overlap else None)
         opt.step_count += 1
+        self.store.version += 1
         if self.env.inner_dp > 1:
             # every GPU of the worker updated its shard; replicate master and snapshot
             self.inner_comm.all_gather_flat(master, self.shards, self.env.inner_rank)

@@ -64,6 +64,7 @@ class TrainArgs:
     offload_snapshot: bool = False
     legacy_grad_sum: bool = False
     activation_checkpointing: bool = False
+    fp8: bool = False              # fp8 e4m3/e5m2 decoder projections (GPU, bf16 compute)
     checkpoint_dir: Optional[str] = None
     checkpoint_every: int = 0      # in outer steps (0 = only at the end when checkpoint_dir is set)
     stop_at_step: int = 0          # stop early (simulated preemption) after this inner step; 0 = run to total
@@ -118,7 +119,8 @@ class Trainer:
         self.outer_steps = a.total_steps // a.inner_steps
         self.compute_dtype = _dtype(a.dtype, e.device)
         self.model = LlamaForCausalLM(self.llama_config, e.device, self.compute_dtype,
-                                      activation_checkpointing=a.activation_checkpointing).init_weights(a.seed)
+                                      activation_checkpointing=a.activation_checkpointing,
+                                      fp8=a.fp8).init_weights(a.seed)
         inner = FlatAdamW(self.model.store, lr=a.lr, weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm,
                           skip_nonfinite=a.skip_nonfinite)
         outer = FlatOuterNesterov(self.model.store, lr=a.outer_lr, momentum=a.outer_momentum)
