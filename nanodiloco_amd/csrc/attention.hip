@@ -50,14 +50,12 @@ __device__ __forceinline__ bf16x8 cat4(sv4 a, sv4 b) {
 
 // Pack accumulator registers 8s..8s+7 into a bf16 MFMA operand fragment.
 __device__ __forceinline__ bf16x8 pack_frag(const f32x16& x, int s) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    const uint32_t u = pack2(x[8 * s + j], x[8 * s + j + 1]);
-    r[j] = (short)(u & 0xffff);
-    r[j + 1] = (short)(u >> 16);
-  }
-  return r;
+  u32x4 u;
+  u[0] = pack2(x[8 * s + 0], x[8 * s + 1]);
+  u[1] = pack2(x[8 * s + 2], x[8 * s + 3]);
+  u[2] = pack2(x[8 * s + 4], x[8 * s + 5]);
+  u[3] = pack2(x[8 * s + 6], x[8 * s + 7]);
+  return __builtin_bit_cast(bf16x8, u);
 }
 
 __device__ __forceinline__ bf16x8 load16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
@@ -269,7 +267,7 @@ __device__ __forceinline__ void store_T(bf16_t* out_row, f32x16* acc, float mul,
 
 // =============================================================================== forward
 template <int HD, bool ROPE>
-__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int nh, int nkv, int T,
                                                           int64_t ld, int64_t ldo, float scale,
@@ -317,12 +315,19 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_fwd_kernel(cons
     const bf16_t* Kt = Ks + (j & 1) * (BN * HD);
     const bf16_t* Vt = Vs + (j & 1) * (BN * HD);
     if (k0 <= q0w + 31) {  // else: whole tile above this wave's diagonal (wave-uniform)
+      // K row fragments issued up front (V^T transposing reads stay next to their MFMAs: holding
+      // them too costs the third wave per SIMD)
+      bf16x8 ka[2][NT];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) ka[kt][t] = row_frag<HD>(Kt, kt * 32 + c32, t, h);
       f32x16 s[2];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         s[kt] = f32x16{};
 #pragma unroll
-        for (int t = 0; t < NT; ++t) s[kt] = mfma32(row_frag<HD>(Kt, kt * 32 + c32, t, h), qf[t], s[kt]);
+        for (int t = 0; t < NT; ++t) s[kt] = mfma32(ka[kt][t], qf[t], s[kt]);
       }
       if ((k0 + BN - 1 > q0w) || (k0 + BN > T)) {
 #pragma unroll
@@ -470,38 +475,45 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
     const bf16_t* Kt = Ks + (j & 1) * (BN * HD);
     const bf16_t* Vt = Vs + (j & 1) * (BN * HD);
     if (k0 <= q0w + 31) {
-      f32x16 s[2], dp[2];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        s[kt] = f32x16{};
-        dp[kt] = f32x16{};
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          s[kt] = mfma32(row_frag<HD>(Kt, kt * 32 + c32, t, h), qf[t], s[kt]);
-          dp[kt] = mfma32(row_frag<HD>(Vt, kt * 32 + c32, t, h), dof[t], dp[kt]);
-        }
-      }
       const bool diag = (k0 + BN - 1 > q0w) || (k0 + BN > T) || (qi >= T);
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt) {
+        if (k0 + kt * 32 > q0w + 31) continue;  // this 32-key half is above the wave's diagonal
+        // fragments issued up front (row reads for S^T / dP^T, transposing reads for dQ)
+        bf16x8 ka[NT], va[NT], tk[2][NO];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float p = fexp2(fmaf(s[kt][r], c, -lse));
-          if (diag) {
-            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (!(key <= qi && key < T && qi < T)) p = 0.f;
-          }
-          dp[kt][r] = p * (dp[kt][r] - dlt);
+        for (int t = 0; t < NT; ++t) {
+          ka[t] = row_frag<HD>(Kt, kt * 32 + c32, t, h);
+          va[t] = row_frag<HD>(Vt, kt * 32 + c32, t, h);
         }
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+        for (int sidx = 0; sidx < 2; ++sidx)
+#pragma unroll
+          for (int o = 0; o < NO; ++o) tk[sidx][o] = tr_frag<HD>(Kt, kt * 32 + 16 * sidx, o * 32, g, i16);
+        f32x16 s = f32x16{}, dp = f32x16{};
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          s = mfma32(ka[t], qf[t], s);
+          dp = mfma32(va[t], dof[t], dp);
+        }
+        if (!diag) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dp[r] = fexp2(fmaf(s[r], c, -lse)) * (dp[r] - dlt);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float p = (key <= qi && key < T && qi < T) ? fexp2(fmaf(s[r], c, -lse)) : 0.f;
+            dp[r] = p * (dp[r] - dlt);
+          }
+        }
 #pragma unroll
         for (int sidx = 0; sidx < 2; ++sidx) {
-          const bf16x8 dsf = pack_frag(dp[kt], sidx);
+          const bf16x8 dsf = pack_frag(dp, sidx);
 #pragma unroll
-          for (int o = 0; o < NO; ++o)
-            dq[o] = mfma32(tr_frag<HD>(Kt, kt * 32 + 16 * sidx, o * 32, g, i16), dsf, dq[o]);
+          for (int o = 0; o < NO; ++o) dq[o] = mfma32(tk[sidx][o], dsf, dq[o]);
         }
+      }
     }
     if (j + 1 < ntiles) {
       sk.store(Ks + ((j + 1) & 1) * (BN * HD));
@@ -568,11 +580,11 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
     const int q0 = qstart + (it % ntq) * BQ;
     load_tile<ROPE>(sq, Q + (int64_t)b * T * ld + (int64_t)head * HD, ld, q0, T, cosT, sinT);
     sd.load(dO + (int64_t)b * T * ldo + (int64_t)head * HD, ldo, q0, T);
-    if (threadIdx.x < BQ) {
+    if (threadIdx.x < BQ) {  // stored negated: they seed the S / dP accumulators
       const int qq = q0 + threadIdx.x;
       const int64_t rs = ((int64_t)b * nh + head) * T;
-      lse_n = qq < T ? LSE[rs + qq] / c : 0.f;
-      del_n = qq < T ? DELTA[rs + qq] : 0.f;
+      lse_n = qq < T ? -LSE[rs + qq] / c : 0.f;
+      del_n = qq < T ? -DELTA[rs + qq] : 0.f;
     }
   };
   auto commit = [&](int buf) {
@@ -598,28 +610,53 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
     for (int qs = 0; qs < BQ / 32; ++qs) {
       const int qsub = q0 + qs * 32;
       if (kw0 > qsub + 31 || kw0 >= T) continue;  // wave-uniform: no query >= any of our keys
-      f32x16 s, dp;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qr = qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        s[r] = -lt[qr];
-        dp[r] = -dt[qr];
-      }
+      // All LDS fragments of this step are issued up front (row reads for S / dP, transposing reads
+      // for dV / dK) so their latency hides behind the MFMA chains and the softmax VALU instead of
+      // being exposed one s_waitcnt at a time.
+      bf16x8 qa[NT], da[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        s = mfma32(row_frag<HD>(Qt, qs * 32 + c32, t, h), kf[t], s);
-        dp = mfma32(row_frag<HD>(dOt, qs * 32 + c32, t, h), vf[t], dp);
+        qa[t] = row_frag<HD>(Qt, qs * 32 + c32, t, h);
+        da[t] = row_frag<HD>(dOt, qs * 32 + c32, t, h);
+      }
+      f32x16 s, dp;  // seeded with -LSE / c and -delta of each query row
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int qr = qs * 32 + 8 * r4 + 4 * h;
+        const float4 l4 = *reinterpret_cast<const float4*>(lt + qr);
+        const float4 d4 = *reinterpret_cast<const float4*>(dt + qr);
+        s[4 * r4 + 0] = l4.x; s[4 * r4 + 1] = l4.y; s[4 * r4 + 2] = l4.z; s[4 * r4 + 3] = l4.w;
+        dp[4 * r4 + 0] = d4.x; dp[4 * r4 + 1] = d4.y; dp[4 * r4 + 2] = d4.z; dp[4 * r4 + 3] = d4.w;
+      }
+      bf16x8 tdo[2][NO], tq[2][NO];
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx)
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+          tdo[sidx][o] = tr_frag<HD>(dOt, qs * 32 + 16 * sidx, o * 32, g, i16);
+          tq[sidx][o] = tr_frag<HD>(Qt, qs * 32 + 16 * sidx, o * 32, g, i16);
+        }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        s = mfma32(qa[t], kf[t], s);
+        dp = mfma32(da[t], vf[t], dp);
       }
       const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T);
+      if (!diag) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = fexp2(s[r] * c);
-        if (diag) {
-          const int qq = qsub + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (!(key <= qq && qq < T && key < T)) p = 0.f;
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(s[r] * c);
+          s[r] = p;
+          dp[r] = p * dp[r];
         }
-        s[r] = p;
-        dp[r] = p * dp[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qq = qsub + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float p = (key <= qq && qq < T && key < T) ? fexp2(s[r] * c) : 0.f;
+          s[r] = p;
+          dp[r] = p * dp[r];
+        }
       }
 #pragma unroll
       for (int sidx = 0; sidx < 2; ++sidx) {
@@ -627,8 +664,8 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
         const bf16x8 dsf = pack_frag(dp, sidx);
 #pragma unroll
         for (int o = 0; o < NO; ++o) {
-          dv[o] = mfma32(tr_frag<HD>(dOt, qs * 32 + 16 * sidx, o * 32, g, i16), pf, dv[o]);
-          dk[o] = mfma32(tr_frag<HD>(Qt, qs * 32 + 16 * sidx, o * 32, g, i16), dsf, dk[o]);
+          dv[o] = mfma32(tdo[sidx][o], pf, dv[o]);
+          dk[o] = mfma32(tq[sidx][o], dsf, dk[o]);
         }
       }
     }

@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(const bf16_t* __restrict_
   const int tn_count = (N + BN - 1) / BN;
   const int tiles = ((M + BM - 1) / BM) * tn_count;
   const int id = xcd_remap(blockIdx.x, tiles * S);
-  const int tile = id / S, split = id % S;
+  const int split = id / tiles, tile = id % tiles;  // one XCD: same K range, neighbouring tiles (L2 reuse)
   const int m0 = (tile / tn_count) * BM, n0 = (tile % tn_count) * BN;
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(512, 2) wgrad256_kernel(const bf16_t* __restri
   const int tn_count = (N + BN2 - 1) / BN2;
   const int tiles = ((M + BM2 - 1) / BM2) * tn_count;
   const int id = xcd_remap(blockIdx.x, tiles * S);
-  const int tile = id / S, split = id % S;
+  const int split = id / tiles, tile = id % tiles;  // one XCD: same K range, neighbouring tiles (L2 reuse)
   const int m0 = (tile / tn_count) * BM2, n0 = (tile % tn_count) * BN2;
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
@@ -345,7 +345,7 @@ __global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restr
   const int tn_count = (N + BN2 - 1) / BN2;
   const int tiles = ((M + BM2 - 1) / BM2) * tn_count;
   const int id = xcd_remap(blockIdx.x, tiles * S);
-  const int tile = id / S, split = id % S;
+  const int split = id / tiles, tile = id % tiles;  // one XCD: same K range, neighbouring tiles (L2 reuse)
   const int m0 = (tile / tn_count) * BM2, n0 = (tile % tn_count) * BN2;
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
@@ -430,6 +430,265 @@ __global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restr
     }
 }
 
+
+
+// ---------------------------------------------------------------------------------------------
+// 16x16x32 variant of the LDS-DMA kernel.  On random data the chip holds a higher clock on
+// v_mfma_f32_16x16x32_bf16 loops than on 32x32x16 ones at equal cycles per FLOP (MI355X_MICROARCH
+// 'clock', item 7), so the same 256 x 256 tile is computed as 8 x 4 16x16 tiles per wave.
+// A 16x16x32 fragment needs k rows 0-3 / 8-11 in one 32-lane half, so the swizzle also folds row bit
+// 3 into chunk bit 1:  phys_chunk = chunk ^ ((row & 3) << 2 | ((row >> 3) & 1) << 1)  (conflict-free
+// for the transposing reads; applied on the DMA source address as before).
+namespace {
+__device__ __forceinline__ int swz16(int row) { return ((row & 3) << 2) | (((row >> 3) & 1) << 1); }
+__device__ __forceinline__ int toff16(int row, int col) {
+  return row * 256 + (((col >> 3) ^ swz16(row)) << 3) + (col & 7);
+}
+// lane l: column cbase + (l & 15), k rows kbase + 8 (l >> 4) + 0..7
+__device__ __forceinline__ bf16x8 frag16(const bf16_t* tile, int kbase, int cbase, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = kbase + 8 * g + (i >> 2);
+  const int col = cbase + 4 * (i & 3);
+  const sv4 lo = tr_read(&tile[toff16(row, col)]);
+  const sv4 hi = tr_read(&tile[toff16(row + 4, col)]);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bfv8, a), __builtin_bit_cast(bfv8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ void dma_tile16(bf16_t* tile, const bf16_t* base, int64_t ld, int k0, int c0, int cols) {
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t tile_addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)tile);
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int pair = w + 8 * it;
+    const int row = 2 * pair + (lane >> 5);
+    const int c = (lane & 31) ^ swz16(row);
+    int col = c0 + c * 8;
+    col = col < cols ? col : cols - 8;
+    glds16(base + (int64_t)(k0 + row) * ld + col, __builtin_amdgcn_readfirstlane(tile_addr + pair * 1024));
+  }
+}
+__device__ __forceinline__ void reg_tile16(bf16_t* tile, const bf16_t* base, int64_t ld, int k0, int kend, int c0,
+                                           int cols) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int c = threadIdx.x + it * 512;
+    const int row = c >> 5, ch = c & 31;
+    const int k = k0 + row, col = c0 + ch * 8;
+    bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (k < kend && col < cols) v = *reinterpret_cast<const bf16x8*>(base + (int64_t)k * ld + col);
+    *reinterpret_cast<bf16x8*>(&tile[toff16(row, ch * 8)]) = v;
+  }
+}
+}  // namespace
+
+__global__ void __launch_bounds__(512, 2) wgrad_m16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                           float* __restrict__ C, float* __restrict__ slab, int M,
+                                                           int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
+                                                           int kchunk) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  constexpr int TA = BK3 * BM2, TB = BK3 * BN2;
+  const int tn_count = (N + BN2 - 1) / BN2;
+  const int tiles = ((M + BM2 - 1) / BM2) * tn_count;
+  const int id = xcd_remap(blockIdx.x, tiles * S);
+  const int split = id / tiles, tile = id % tiles;  // one XCD: same K range, neighbouring tiles (L2 reuse)
+  const int m0 = (tile / tn_count) * BM2, n0 = (tile % tn_count) * BN2;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 2, wn = w & 3;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kend > kbeg ? (kend - kbeg + BK3 - 1) / BK3 : 0;
+  auto stage = [&](int kt) {
+    bf16_t* ta = smem + (kt & 1) * (TA + TB);
+    bf16_t* tb = ta + TA;
+    const int k0 = kbeg + kt * BK3;
+    if (k0 + BK3 <= kend) {
+      dma_tile16(ta, A, lda, k0, m0, M);
+      dma_tile16(tb, B, ldb, k0, n0, N);
+    } else {
+      reg_tile16(ta, A, lda, k0, kend, m0, M);
+      reg_tile16(tb, B, ldb, k0, kend, n0, N);
+    }
+  };
+  if (nk > 0) stage(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) stage(kt + 1);
+    const bf16_t* a_t = smem + (kt & 1) * (TA + TB);
+    const bf16_t* b_t = a_t + TA;
+#pragma unroll
+    for (int ks = 0; ks < BK3 / 32; ++ks) {
+      bf16x8 fa[8], fb[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) fb[b] = frag16(b_t, ks * 32, wn * 64 + b * 16, lane);
+#pragma unroll
+      for (int a = 0; a < 8; ++a) fa[a] = frag16(a_t, ks * 32, wm * 128 + a * 16, lane);
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = mfma16(fa[a], fb[b], acc[a][b]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  float* out = S == 1 ? C : slab + (int64_t)split * M * N;
+  const int64_t ldo = S == 1 ? ldc : N;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int n = n0 + wn * 64 + b * 16 + (lane & 15);
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 128 + a * 16 + 4 * (lane >> 4) + r;
+        if (m < M) {
+          float* p = out + (int64_t)m * ldo + n;
+          if (S == 1) *p += acc[a][b][r];
+          else *p = acc[a][b][r];
+        }
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ring variant: the LDS-DMA kernel above waits vmcnt(0) + barrier every K tile, so each tile's DMA
+// must land within ONE tile of MFMAs.  Here the 128 KiB of LDS is a NBUF-deep ring of BK = 32 tiles
+// and the DMA runs NBUF-1 tiles ahead behind a COUNTED vmcnt (never 0 in the steady state):
+//   vmcnt(P * in_flight_after_kt) | barrier | DMA tile kt+NBUF-1 -> slot (kt-1) % NBUF | 16 MFMAs on slot kt
+// One barrier per tile both publishes tile kt (everyone's DMA landed) and retires slot kt-1 (everyone's
+// reads of it returned before their MFMAs issued).  P = 4 DMA wave-instructions per tile per wave.
+// Used when K is a multiple of 32 within every split (no tail tile).
+namespace {
+constexpr int BKR = 32;
+
+__device__ __forceinline__ void dma_tile32(uint32_t tile_addr, const bf16_t* base, int64_t ld, int k0, int c0,
+                                           int cols) {
+  // 32 rows x 512 B = 16 wave-instructions of 1 KiB; wave w issues row pairs w and w + 8
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int pair = w + 8 * it;
+    const int row = 2 * pair + (lane >> 5);
+    const int p = lane & 31;
+    const int c = p ^ ((row & 3) << 2);
+    int col = c0 + c * 8;
+    col = col < cols ? col : cols - 8;
+    glds16(base + (int64_t)(k0 + row) * ld + col, __builtin_amdgcn_readfirstlane(tile_addr + pair * 1024));
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
+}
+}  // namespace
+
+template <int NBUF>
+__global__ void __launch_bounds__(512, 1) wgrad_ring_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                            float* __restrict__ C, float* __restrict__ slab, int M,
+                                                            int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
+                                                            int kchunk) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  constexpr int TA = BKR * BM2, TB = BKR * BN2;  // elements per operand tile
+  constexpr int SLOT_BYTES = (TA + TB) * 2;
+  constexpr int P = 4;                            // DMA wave-instructions per tile per wave
+  const int tn_count = (N + BN2 - 1) / BN2;
+  const int tiles = ((M + BM2 - 1) / BM2) * tn_count;
+  const int id = xcd_remap(blockIdx.x, tiles * S);
+  const int split = id / tiles, tile = id % tiles;  // one XCD: same K range, neighbouring tiles (L2 reuse)
+  const int m0 = (tile / tn_count) * BM2, n0 = (tile % tn_count) * BN2;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int wm = w >> 2, wn = w & 3;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)smem);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+
+  const int nk = kend > kbeg ? (kend - kbeg) / BKR : 0;
+  auto stage = [&](int kt) {
+    const uint32_t base = lds0 + (uint32_t)((kt % NBUF) * SLOT_BYTES);
+    const int k0 = kbeg + kt * BKR;
+    dma_tile32(base, A, lda, k0, m0, M);
+    dma_tile32(base + TA * 2, B, ldb, k0, n0, N);
+  };
+#pragma unroll
+  for (int j = 0; j < NBUF - 1; ++j)
+    if (j < nk) stage(j);
+  for (int kt = 0; kt < nk; ++kt) {
+    // tiles issued after kt that may still be in flight: min(NBUF-2, nk-1-kt)
+    const int after = min(NBUF - 2, nk - 1 - kt);
+    if (after >= 2) wait_vm<2 * P>();
+    else if (after == 1) wait_vm<P>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + NBUF - 1 < nk) stage(kt + NBUF - 1);
+    const bf16_t* a_t = smem + (kt % NBUF) * (TA + TB);
+    const bf16_t* b_t = a_t + TA;
+    bf16x8 fa[2][4], fb[2][2];
+#pragma unroll
+    for (int ks = 0; ks < BKR / 16; ++ks) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) fb[ks][b] = frag2(b_t, ks * 16, wn * 64 + b * 32, g, i16);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) fa[ks][a] = frag2(a_t, ks * 16, wm * 128 + a * 32, g, i16);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < BKR / 16; ++ks)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(fa[ks][a], fb[ks][b], acc[a][b]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // k-step 0's reads
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {                         // k-step 1's reads overlap k-step 0's MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);
+  }
+  float* out = S == 1 ? C : slab + (int64_t)split * M * N;
+  const int64_t ldo = S == 1 ? ldc : N;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int n = n0 + wn * 64 + b * 32 + c32;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M) {
+          float* p = out + (int64_t)m * ldo + n;
+          if (S == 1) *p += acc[a][b][r];
+          else *p = acc[a][b][r];
+        }
+      }
+    }
+}
+
 // C[m][n] += sum_s slab[s][m][n]   (fixed summation order)
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ C, int M,
                                                           int N, int64_t ldc, int S) {
@@ -488,9 +747,28 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
   // ND_WGRAD_VARIANT (A/B runs): "reg" register-staged 256 kernel, "dma0" LDS-DMA without the
   // sched_group_barrier interleave; default: LDS-DMA with the interleave.
   const char* ev = getenv("ND_WGRAD_VARIANT");
-  const int variant = (ev && ev[0] == 'r') ? 1 : 0;
+  const int variant = (ev && ev[0] == 'r') ? 1 : (ev && ev[0] == 'p') ? 2 : (ev && ev[0] == 'm') ? 3 : 0;
   const bool sched = !(ev && ev[0] == 'd' && ev[3] == '0');
-  if (large && variant == 0 && M >= 8 && N >= 8) {
+  const int kchunk_r = ((K + S - 1) / S + BKR - 1) / BKR * BKR;
+  if (large && variant == 2 && K % BKR == 0) {
+    const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
+    constexpr int NB = 4;
+    const size_t lds = (size_t)NB * BKR * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB
+    static const hipError_t attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_ring_kernel<NB>),
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)attr_ok;
+    hipLaunchKernelGGL(wgrad_ring_kernel<NB>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
+                       C, slab, M, N, K, lda, ldb, ldc, S, kchunk_r);
+  } else if (large && variant == 3) {
+    const int kchunk = ((K + S - 1) / S + BK3 - 1) / BK3 * BK3;
+    const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
+    const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB
+    static const hipError_t attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_m16_kernel),
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)attr_ok;
+    hipLaunchKernelGGL(wgrad_m16_kernel, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B, C,
+                       slab, M, N, K, lda, ldb, ldc, S, kchunk);
+  } else if (large && variant != 1 && M >= 8 && N >= 8) {
     const int kchunk = ((K + S - 1) / S + BK3 - 1) / BK3 * BK3;
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB

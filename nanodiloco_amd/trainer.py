@@ -49,7 +49,7 @@ class TrainArgs:
     llama_config_file: Optional[str] = None
     wandb_config_file: Optional[str] = None
     # ---- extensions
-    dtype: str = "auto"            # auto | fp32 | bf16
+    dtype: str = "auto"            # auto | fp32 | bf16 | fp8 (= bf16 compute + fp8 decoder projections)
     data: str = "auto"             # auto | synthetic | memmap | hf
     ops: str = "auto"              # auto | hip | torch
     backend: str = "auto"          # auto | nccl | gloo
@@ -86,7 +86,7 @@ def _dtype(name: str, device: torch.device) -> torch.dtype:
     if name == "auto":
         return torch.bfloat16 if device.type == "cuda" else torch.float32
     return {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
-            "bfloat16": torch.bfloat16}[name]
+            "bfloat16": torch.bfloat16, "fp8": torch.bfloat16}[name]
 
 
 def _resolve_data_kind(a: TrainArgs) -> str:
@@ -120,7 +120,7 @@ class Trainer:
         self.compute_dtype = _dtype(a.dtype, e.device)
         self.model = LlamaForCausalLM(self.llama_config, e.device, self.compute_dtype,
                                       activation_checkpointing=a.activation_checkpointing,
-                                      fp8=a.fp8).init_weights(a.seed)
+                                      fp8=a.fp8 or a.dtype == "fp8").init_weights(a.seed)
         inner = FlatAdamW(self.model.store, lr=a.lr, weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm,
                           skip_nonfinite=a.skip_nonfinite)
         outer = FlatOuterNesterov(self.model.store, lr=a.outer_lr, momentum=a.outer_momentum)
