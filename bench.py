@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--inner-steps", type=int, default=100)
     ap.add_argument("--inner-dp", type=int, default=1)
     ap.add_argument("--ops", default="auto", choices=["auto", "hip", "torch"])
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="collective backend (auto = nccl/RCCL on GPU); gloo lets several ranks share one GPU")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--bucket-mb", type=float, default=128.0)
     ap.add_argument("--overlap-outer", action="store_true")
@@ -64,7 +66,7 @@ def parse():
 def main():
     a = parse()
     ops.set_backend(a.ops)
-    env = init_distributed("auto", a.inner_dp)
+    env = init_distributed(a.backend, a.inner_dp)
     if env.world_size != a.gpus and env.rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
     cfg = resolve_llama_config(a.model)
