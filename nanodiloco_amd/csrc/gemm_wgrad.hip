@@ -304,6 +304,48 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte_addr)
       : "memory");
 }
 
+// saddr form: 64-bit uniform base in SGPRs + 32-bit per-lane byte offset (no per-lane 64-bit math).
+__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32_t lds_byte_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_byte_addr)
+      : "memory");
+}
+
+// Per-lane DMA source offsets of a 64 x 256 operand tile, computed once per kernel: the tile at
+// K offset k0 is then 4 wave-instructions from the uniform base  base + (k0 + 16 it) * ld,
+// with the same per-lane byte offset (row-in-pair * ld + swizzled, clamped column) * 2.
+struct DmaPlan {
+  uint32_t voff;   // per-lane byte offset inside a row pair
+  uint32_t lds0;   // wave's first 1-KiB destination (pair w) relative to the tile base
+  __device__ __forceinline__ void init(int64_t ld, int c0, int cols) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int rp = lane >> 5;                       // row inside the pair (rows 2 pair + rp)
+    const int p = lane & 31;
+    // row & 3 == (2 w + rp) & 3 for every it (rows advance by 16)
+    const int c = p ^ (((2 * w + rp) & 3) << 2);
+    int col = c0 + c * 8;
+    col = col < cols ? col : cols - 8;
+    voff = (uint32_t)(((int64_t)rp * ld + col) * 2);
+    lds0 = (uint32_t)(w * 1024);
+  }
+  // rows 2w + 16 it + {0,1} of tile k0 -> LDS tile at byte address tile_addr
+  __device__ __forceinline__ void issue(const bf16_t* base, int64_t ld, int k0, uint32_t tile_addr) const {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const bf16_t* sb = base + (int64_t)(k0 + 2 * w + 16 * it) * ld;
+      glds16s(sb, voff, tile_addr + (uint32_t)((w + 8 * it) * 1024));
+    }
+  }
+};
+
 __device__ __forceinline__ void dma_tile(bf16_t* tile, const bf16_t* base, int64_t ld, int k0, int c0, int cols) {
   // 64 rows x 512 B = 32 wave-instructions of 1 KiB; wave w issues rows (2i, 2i+1) for i = w, w+8, w+16, w+24
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -335,7 +377,7 @@ __device__ __forceinline__ void reg_tile(bf16_t* tile, const bf16_t* base, int64
 }
 }  // namespace
 
-template <bool SCHED>
+template <bool SCHED, bool NODMA = false>  // NODMA: diagnostic only (skips the loads; garbage result)
 __global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                            float* __restrict__ C, float* __restrict__ slab, int M,
                                                            int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
@@ -359,13 +401,19 @@ __global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restr
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
 
   const int nk = kend > kbeg ? (kend - kbeg + BK3 - 1) / BK3 : 0;
+  DmaPlan pa, pb;
+  pa.init(lda, m0, M);
+  pb.init(ldb, n0, N);
+  const uint32_t lds_base = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)smem);
   auto stage = [&](int kt) {
+    if (NODMA) return;
     bf16_t* ta = smem + (kt & 1) * (TA + TB);
     bf16_t* tb = ta + TA;
     const int k0 = kbeg + kt * BK3;
     if (k0 + BK3 <= kend) {
-      dma_tile(ta, A, lda, k0, m0, M);
-      dma_tile(tb, B, ldb, k0, n0, N);
+      const uint32_t la = lds_base + (uint32_t)((kt & 1) * (TA + TB) * 2);
+      pa.issue(A, lda, k0, la);
+      pb.issue(B, ldb, k0, la + TA * 2);
     } else {
       reg_tile(ta, A, lda, k0, kend, m0, M);
       reg_tile(tb, B, ldb, k0, kend, n0, N);
@@ -747,7 +795,8 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
   // ND_WGRAD_VARIANT (A/B runs): "reg" register-staged 256 kernel, "dma0" LDS-DMA without the
   // sched_group_barrier interleave; default: LDS-DMA with the interleave.
   const char* ev = getenv("ND_WGRAD_VARIANT");
-  const int variant = (ev && ev[0] == 'r') ? 1 : (ev && ev[0] == 'p') ? 2 : (ev && ev[0] == 'm') ? 3 : 0;
+  const int variant = (ev && ev[0] == 'r') ? 1 : (ev && ev[0] == 'p') ? 2 : (ev && ev[0] == 'm') ? 3
+                      : (ev && ev[0] == 'n') ? 4 : 0;
   const bool sched = !(ev && ev[0] == 'd' && ev[3] == '0');
   const int kchunk_r = ((K + S - 1) / S + BKR - 1) / BKR * BKR;
   if (large && variant == 2 && K % BKR == 0) {
@@ -759,6 +808,15 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
     (void)attr_ok;
     hipLaunchKernelGGL(wgrad_ring_kernel<NB>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
                        C, slab, M, N, K, lda, ldb, ldc, S, kchunk_r);
+  } else if (large && variant == 4) {  // "nodma": compute-only diagnostic
+    const int kchunk = ((K + S - 1) / S + BK3 - 1) / BK3 * BK3;
+    const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
+    const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);
+    static const hipError_t attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_dma_kernel<true, true>),
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)attr_ok;
+    hipLaunchKernelGGL((wgrad_dma_kernel<true, true>), dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A,
+                       (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
   } else if (large && variant == 3) {
     const int kchunk = ((K + S - 1) / S + BK3 - 1) / BK3 * BK3;
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
