@@ -59,6 +59,7 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=128.0)
     ap.add_argument("--overlap-outer", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
+    ap.add_argument("--fp8-wgrad", action="store_true", help="with --fp8: weight-gradient GEMM in fp8 too")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
     return ap.parse_args()
 
@@ -71,7 +72,7 @@ def main():
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
     cfg = resolve_llama_config(a.model)
     dtype = torch.bfloat16 if env.device.type == "cuda" else torch.float32
-    model = LlamaForCausalLM(cfg, env.device, dtype, fp8=a.fp8).init_weights(1337)
+    model = LlamaForCausalLM(cfg, env.device, dtype, fp8=a.fp8, fp8_wgrad=a.fp8_wgrad).init_weights(1337)
     inner = FlatAdamW(model.store, lr=4e-4)
     outer = FlatOuterNesterov(model.store, lr=0.7, momentum=0.9)
     comm_dtype = torch.bfloat16 if a.comm_dtype == "bf16" else torch.float32

@@ -81,3 +81,73 @@ ND_API int nd_fp8_cast(const void* x, int xdt, int64_t n, const float* scale, vo
   }
   ND_LAUNCH_CHECK();
 }
+
+// Cast + transpose in one pass (fp8 weight-gradient GEMM operands): x [rows, cols] (row stride ld)
+// -> out [rows, cols] (optional, row-major) and outT [cols, rows] (row-major), both fp8(x * scale),
+// plus amax.  64 x 64 tile per 256-thread block: each thread loads 2 x 8 consecutive elements
+// (16-B bf16 loads), writes them straight to `out`, and parks the fp8 bytes in LDS; the transposed
+// tile is then written as 16-B rows of outT (16 consecutive source rows of one column per thread).
+// rows and cols must be multiples of 64 (checked by the caller).
+template <int XDT, int FMT>
+__global__ void __launch_bounds__(256) fp8_cast_t_kernel(const void* __restrict__ x, int rows, int cols, int64_t ld,
+                                                         const float* __restrict__ scale_p, uint8_t* __restrict__ out,
+                                                         uint8_t* __restrict__ outT, float* __restrict__ amax_out,
+                                                         int amax_parts) {
+  __shared__ uint8_t tile[64][64 + 16];
+  const float scale = scale_p ? scale_p[0] : 1.f;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int t = threadIdx.x;
+  float amax = 0.f;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int idx = t + it * 256;          // 512 vectors of 8 elements
+    const int r = idx >> 3, cv = (idx & 7) * 8;
+    float v[8];
+    Vec8<XDT>::load(x, (int64_t)(r0 + r) * ld + c0 + cv, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+    uint2 o;
+    o.x = cvt4<FMT>(v[0] * scale, v[1] * scale, v[2] * scale, v[3] * scale);
+    o.y = cvt4<FMT>(v[4] * scale, v[5] * scale, v[6] * scale, v[7] * scale);
+    if (out) *reinterpret_cast<uint2*>(out + (int64_t)(r0 + r) * cols + c0 + cv) = o;
+    *reinterpret_cast<uint2*>(&tile[r][cv]) = o;
+  }
+  __syncthreads();
+  {
+    const int c = t >> 2, rq = (t & 3) * 16;  // column c, source rows rq .. rq+15
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      w[q] = (uint32_t)tile[rq + 4 * q][c] | ((uint32_t)tile[rq + 4 * q + 1][c] << 8) |
+             ((uint32_t)tile[rq + 4 * q + 2][c] << 16) | ((uint32_t)tile[rq + 4 * q + 3][c] << 24);
+    }
+    *reinterpret_cast<uint4*>(outT + (int64_t)(c0 + c) * rows + r0 + rq) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  if (amax_out) {
+    __shared__ float red[4];
+    amax = wave_max(amax);
+    if ((t & 63) == 0) red[t >> 6] = amax;
+    __syncthreads();
+    if (t == 0) {
+      amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      const int b = blockIdx.y * gridDim.x + blockIdx.x;
+      atomicMax(reinterpret_cast<int*>(amax_out + b % amax_parts), __float_as_int(amax));
+    }
+  }
+}
+
+ND_API int nd_fp8_cast_t(const void* x, int xdt, int rows, int cols, int64_t ld, const float* scale, void* out,
+                         void* outT, int fmt, float* amax_out, int amax_parts, hipStream_t s) {
+  if (rows % 64 || cols % 64 || ld % 8 || outT == nullptr) return (int)hipErrorInvalidValue;
+  if (amax_parts < 1) amax_parts = 1;
+  const dim3 g(cols / 64, rows / 64), b(256);
+  uint8_t *o = (uint8_t*)out, *oT = (uint8_t*)outT;
+  if (xdt == BF16) {
+    if (fmt == 0) hipLaunchKernelGGL((fp8_cast_t_kernel<BF16, 0>), g, b, 0, s, x, rows, cols, ld, scale, o, oT, amax_out, amax_parts);
+    else hipLaunchKernelGGL((fp8_cast_t_kernel<BF16, 1>), g, b, 0, s, x, rows, cols, ld, scale, o, oT, amax_out, amax_parts);
+  } else {
+    if (fmt == 0) hipLaunchKernelGGL((fp8_cast_t_kernel<F32, 0>), g, b, 0, s, x, rows, cols, ld, scale, o, oT, amax_out, amax_parts);
+    else hipLaunchKernelGGL((fp8_cast_t_kernel<F32, 1>), g, b, 0, s, x, rows, cols, ld, scale, o, oT, amax_out, amax_parts);
+  }
+  ND_LAUNCH_CHECK();
+}

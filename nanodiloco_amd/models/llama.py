@@ -52,7 +52,8 @@ class _GradHook(torch.autograd.Function):
 
 class LlamaForCausalLM:
     def __init__(self, config: LlamaConfig, device="cpu", compute_dtype: torch.dtype = torch.float32,
-                 store: Optional[ParamStore] = None, activation_checkpointing: bool = False, fp8: bool = False):
+                 store: Optional[ParamStore] = None, activation_checkpointing: bool = False, fp8: bool = False,
+                 fp8_wgrad: bool = False):
         self.config = config
         self.device = torch.device(device)
         self.compute_dtype = compute_dtype
@@ -73,7 +74,7 @@ class LlamaForCausalLM:
             if compute_dtype != torch.bfloat16 or self.device.type != "cuda":
                 raise ValueError("fp8 needs bf16 compute on an MI355X")
             from ..ops.fp8 import Fp8Linears
-            self.fp8 = Fp8Linears(self.device)
+            self.fp8 = Fp8Linears(self.device, wgrad_fp8=fp8_wgrad)
 
     # ------------------------------------------------------------------ init / io
     @torch.no_grad()

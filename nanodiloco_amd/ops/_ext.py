@@ -126,6 +126,7 @@ def _declare(L: ctypes.CDLL):
         "nd_axpby": [P, P, L64, F, F, P],
         # fp8 quantisation
         "nd_fp8_cast": [P, I, L64, P, P, I, P, I, P],
+        "nd_fp8_cast_t": [P, I, I, I, L64, P, P, P, I, P, I, P],
         # weight-gradient GEMM
         "nd_wgrad_splits": [I, I, I],
         "nd_wgrad": [P, P, P, P, I, I, I, L64, L64, L64, P],

@@ -3,8 +3,12 @@
 Recipe (per-tensor scaling, the common "delayed scaling" scheme):
 * forward  ``y = x @ W^T`` with x, W in e4m3 -> hipBLASLt fp8 GEMM (``torch._scaled_mm``), bf16 out;
 * dgrad    ``dx = dy @ W`` with dy in e5m2 (range for gradients), W^T in e4m3;
-* wgrad    stays bf16 on our ``nd_wgrad`` kernel (fp32 accumulate into the flat grad buffer), so the
-  master-weight update sees full-precision gradients;
+* wgrad    ``dW = dy^T x`` as an fp8 GEMM too (e5m2 x e4m3, fp32 out, added into the flat fp32 grad
+  buffer); its K-major operands dy^T / x^T come from ``nd_fp8_cast_t``, which writes the fp8 tensor
+  AND its transpose in one pass -- the forward saves x^T in fp8 (half the bytes of bf16 x).
+  Off by default (``wgrad_fp8=False`` = bf16 ``nd_wgrad``): on the Llama-150M shapes hipBLASLt's fp8
+  kernel for this K = 32768 reduction ran at ~215 us vs ~236 us for our bf16 kernel, which the
+  transposing casts (65-115 us) more than eat (profiles/r1_bench150m_fp8_kernel_stats_v2.md);
 * activations / gradients are quantised by ``nd_fp8_cast`` (one pass: scale, saturate, convert,
   and record amax) with a scale derived from the amax history of previous steps (``Fp8Recipe``;
   device-side, no host sync); the very first use of a tensor role is scaled from its current amax;
@@ -39,6 +43,25 @@ def cast(x: torch.Tensor, scale: torch.Tensor, fmt: int, amax: Optional[torch.Te
     return out
 
 
+def cast_t(x: torch.Tensor, scale: torch.Tensor, fmt: int, amax: Optional[torch.Tensor] = None,
+           want_plain: bool = True):
+    """(fp8(x * scale) or None, its transpose) in one pass; x is [rows, cols] with rows, cols % 64 == 0."""
+    rows, cols = x.shape
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    out = torch.empty(rows, cols, dtype=TORCH_DT[fmt], device=x.device) if want_plain else None
+    outT = torch.empty(cols, rows, dtype=TORCH_DT[fmt], device=x.device)
+    _ext.check(_ext.lib().nd_fp8_cast_t(_ext.ptr(x), _ext.dtcode(x), rows, cols, x.stride(0), _ext.ptr(scale),
+                                        _ext.ptr(out), _ext.ptr(outT), fmt, _ext.ptr(amax),
+                                        amax.numel() if amax is not None else 1, _ext.stream_ptr(x.device)),
+               "nd_fp8_cast_t")
+    return out, outT
+
+
+def _t_ok(x: torch.Tensor) -> bool:
+    return x.dim() == 2 and x.shape[0] % 64 == 0 and x.shape[1] % 64 == 0
+
+
 class Fp8Recipe:
     """Amax history / scale bookkeeping for every quantised tensor role, in a few flat device tensors."""
 
@@ -58,14 +81,25 @@ class Fp8Recipe:
         self.fmax[k] = FMAX[fmt]
         return k
 
-    def quantize(self, x: torch.Tensor, k: int, fmt: int) -> torch.Tensor:
+    def _first_use(self, x: torch.Tensor, k: int):
         if not self.ready[k]:  # first use: current scaling from this tensor's own amax
             a = x.detach().abs().amax().float().clamp_min(1e-30)
             s = self.fmax[k] / (a * 2.0 ** self.margin)
             self.scale[k:k + 1].copy_(s.reshape(1))
             self.inv[k:k + 1].copy_((1.0 / s).reshape(1))
             self.ready[k] = True
+
+    def quantize(self, x: torch.Tensor, k: int, fmt: int) -> torch.Tensor:
+        self._first_use(x, k)
         return cast(x, self.scale[k:k + 1], fmt, self.amax[k])
+
+    def quantize_t(self, x: torch.Tensor, k: int, fmt: int, want_plain: bool = True):
+        """(x8, x8^T) with the slot's scale (falls back to a separate transpose off the fast shapes)."""
+        self._first_use(x, k)
+        if _t_ok(x):
+            return cast_t(x, self.scale[k:k + 1], fmt, self.amax[k], want_plain)
+        q = cast(x, self.scale[k:k + 1], fmt, self.amax[k])
+        return q, q.t().contiguous()
 
     @torch.no_grad()
     def update(self):
@@ -104,33 +138,46 @@ class Fp8Weight:
 
 class Fp8LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, gw, wq: Fp8Weight, recipe: Fp8Recipe, kx: int, kdy: int):
-        x8 = recipe.quantize(x, kx, E4M3)
-        y = torch._scaled_mm(x8, wq.w8.t(), recipe.inv[kx:kx + 1], wq.inv, out_dtype=torch.bfloat16)
-        ctx.save_for_backward(x)
-        ctx.gw, ctx.wq, ctx.recipe, ctx.kdy = gw, wq, recipe, kdy
+    def forward(ctx, x, w, gw, wq: Fp8Weight, recipe: Fp8Recipe, kx: int, kdy: int, wgrad_fp8: bool):
+        if wgrad_fp8:
+            x8, x8t = recipe.quantize_t(x, kx, E4M3)
+            ctx.save_for_backward(x8t)
+        else:
+            x8 = recipe.quantize(x, kx, E4M3)
+            ctx.save_for_backward(x)
+        inv_x = recipe.inv[kx:kx + 1]
+        y = torch._scaled_mm(x8, wq.w8.t(), inv_x, wq.inv, out_dtype=torch.bfloat16)
+        ctx.gw, ctx.wq, ctx.recipe, ctx.kdy, ctx.inv_x, ctx.wgrad_fp8 = gw, wq, recipe, kdy, inv_x, wgrad_fp8
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        (x,) = ctx.saved_tensors
+        (xs,) = ctx.saved_tensors
         dy = dy.contiguous()
         r, k = ctx.recipe, ctx.kdy
-        dy8 = r.quantize(dy, k, E5M2)
-        dx = torch._scaled_mm(dy8, ctx.wq.wT8.t(), r.inv[k:k + 1], ctx.wq.inv, out_dtype=torch.bfloat16)
+        if ctx.wgrad_fp8:
+            dy8, dy8t = r.quantize_t(dy, k, E5M2)
+        else:
+            dy8 = r.quantize(dy, k, E5M2)
+        inv_dy = r.inv[k:k + 1]
+        dx = torch._scaled_mm(dy8, ctx.wq.wT8.t(), inv_dy, ctx.wq.inv, out_dtype=torch.bfloat16)
         if ctx.gw is not None:
-            if wgrad_supported(ctx.gw, dy, x):
-                wgrad(ctx.gw, dy, x)
+            if ctx.wgrad_fp8:
+                # dW[out, in] = dy^T x : mat1 = dy^T (row-major), mat2 = x as column-major [T, in]
+                ctx.gw.add_(torch._scaled_mm(dy8t, xs.t(), inv_dy, ctx.inv_x, out_dtype=torch.float32))
+            elif wgrad_supported(ctx.gw, dy, xs):
+                wgrad(ctx.gw, dy, xs)
             else:
-                ctx.gw.add_(torch.mm(dy.t(), x).float())
-        return dx, None, None, None, None, None, None
+                ctx.gw.add_(torch.mm(dy.t(), xs).float())
+        return dx, None, None, None, None, None, None, None
 
 
 class Fp8Linears:
     """Per-model fp8 state: one recipe, one (x, dy) slot pair and one weight cache per projection."""
 
-    def __init__(self, device):
+    def __init__(self, device, wgrad_fp8: bool = False):
         self.recipe = Fp8Recipe(device)
+        self.wgrad_fp8 = wgrad_fp8
         self.slots: Dict[str, tuple] = {}
         self.weights: Dict[str, Fp8Weight] = {}
 
@@ -140,4 +187,4 @@ class Fp8Linears:
             self.weights[key] = Fp8Weight()
         kx, kdy = self.slots[key]
         wq = self.weights[key].get(w, version)
-        return Fp8LinearFn.apply(x, w, gw, wq, self.recipe, kx, kdy)
+        return Fp8LinearFn.apply(x, w, gw, wq, self.recipe, kx, kdy, self.wgrad_fp8)
