@@ -66,3 +66,43 @@ def test_resume_matches_uninterrupted(tmp_path):
     ra, rb = _log(la), _log(lb)
     assert [x["step"] for x in rb] == [5, 6]
     assert abs(ra[-1]["loss"] - rb[-1]["loss"]) < 1e-5
+
+
+def _bench_json(stdout: str) -> dict:
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout[-2000:]
+    return json.loads(lines[0])
+
+
+BENCH = ["bench.py", "--model", "llama_tiny.json", "--batch-size", "4", "--micro-batch", "2", "--seq-len", "64",
+         "--steps", "3", "--warmup", "1", "--inner-steps", "2"]
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+@pytest.mark.slow
+def test_bench_contract_single_process():
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable] + BENCH + ["--gpus", "1"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _bench_json(r.stdout)
+    assert KEYS <= set(j)
+    assert j["n_gpus"] == 1 and j["steps"] == 3 and j["warmup"] == 1 and j["scaling"] == "weak"
+    assert j["higher_is_better"] is True and j["value"] > 0 and j["data"] == "synthetic"
+    assert abs(j["value"] - 4 * 64 * 3 / (j["ms_per_step"] * 3 / 1000.0)) / j["value"] < 0.01
+    assert j["config"]["global_batch"] == 4 and j["config"]["seq_len"] == 64
+    assert j["outer_steps_in_window"] >= 1
+
+
+@pytest.mark.slow
+def test_bench_contract_two_ranks_gloo():
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port())] + BENCH + ["--gpus", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _bench_json(r.stdout)  # rank 0 only prints
+    assert j["n_gpus"] == 2 and j["config"]["global_batch"] == 8
+    assert j["config"]["parallelism"] == "diloco2"
+    assert j["bytes_per_outer_step"] > 0
