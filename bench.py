@@ -33,6 +33,7 @@ from nanodiloco_amd.data import SyntheticTokens  # noqa: E402
 from nanodiloco_amd.models import LlamaForCausalLM  # noqa: E402
 from nanodiloco_amd.optim import FlatAdamW, FlatOuterNesterov  # noqa: E402
 from nanodiloco_amd.parallel.diloco import Diloco  # noqa: E402
+from nanodiloco_amd.ops.tuned_gemm import enable_tuned_gemms  # noqa: E402
 from nanodiloco_amd.parallel.dist import barrier, init_distributed  # noqa: E402
 from nanodiloco_amd.parallel.inner_ddp import InnerGradSync  # noqa: E402
 
@@ -58,6 +59,7 @@ def parse():
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--bucket-mb", type=float, default=128.0)
     ap.add_argument("--overlap-outer", action="store_true")
+    ap.add_argument("--no-tuned-gemm", action="store_true", help="library-default GEMM algorithms (A/B)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
     ap.add_argument("--fp8-wgrad", action="store_true", help="with --fp8: weight-gradient GEMM in fp8 too")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
@@ -70,6 +72,8 @@ def main():
     env = init_distributed(a.backend, a.inner_dp)
     if env.world_size != a.gpus and env.rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
+    if env.device.type == "cuda" and not a.no_tuned_gemm:
+        enable_tuned_gemms(env.device)
     cfg = resolve_llama_config(a.model)
     dtype = torch.bfloat16 if env.device.type == "cuda" else torch.float32
     model = LlamaForCausalLM(cfg, env.device, dtype, fp8=a.fp8, fp8_wgrad=a.fp8_wgrad).init_weights(1337)
@@ -170,6 +174,7 @@ def main():
             "outer_steps_in_window": n_outer,
             "model_tflops_per_gpu": round(mfu_flops / 1e12, 2),
             "final_loss": round(final_loss, 4),
+            "tuned_gemm": enable_tuned_gemms(env.device) if env.device.type == "cuda" and not a.no_tuned_gemm else False,
             "ops": ops.get_backend() if a.ops != "auto" else ("hip" if env.device.type == "cuda" else "torch"),
         }
         print(json.dumps(out), flush=True)

@@ -65,6 +65,7 @@ class TrainArgs:
     legacy_grad_sum: bool = False
     activation_checkpointing: bool = False
     fp8: bool = False              # fp8 e4m3/e5m2 decoder projections (GPU, bf16 compute)
+    tuned_gemm: bool = True        # load the pre-tuned hipBLASLt algorithm table (ops/tuned_gemm.py)
     checkpoint_dir: Optional[str] = None
     checkpoint_every: int = 0      # in outer steps (0 = only at the end when checkpoint_dir is set)
     stop_at_step: int = 0          # stop early (simulated preemption) after this inner step; 0 = run to total
@@ -112,6 +113,9 @@ class Trainer:
         self.env = env or init_distributed(a.backend, a.inner_dp, device=None if a.device == "auto" else a.device,
                                            timeout_s=a.collective_timeout_s)
         e = self.env
+        if e.device.type == "cuda" and a.tuned_gemm:
+            from .ops.tuned_gemm import enable_tuned_gemms
+            enable_tuned_gemms(e.device)
         self.llama_config: LlamaConfig = resolve_llama_config(a.llama_config_file)
         self.run_config = load_config_from_file(a.wandb_config_file) if a.wandb_config_file else default_run_config()
         set_seed_all(a.seed)
