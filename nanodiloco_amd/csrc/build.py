@@ -112,12 +112,53 @@ def build(force: bool = False, jobs: int = 0, save_temps: bool = False, verbose:
     return {"kernels": kern, "runtime": rt, "compiled": [os.path.basename(s) for s, _ in todo]}
 
 
+def build_revision(rev: str, jobs: int = 0) -> str:
+    """Build libnd_kernels.so from the csrc/ of git revision `rev` into _lib/alt/ (for in-process
+    A/B against the working tree: device-to-device and run-to-run variance on MI355X is several
+    percent, so code versions are compared interleaved inside one process; see scripts/ab_kernels.py)."""
+    import tempfile
+    root = os.path.dirname(PKG)
+    sha = _run(["git", "-C", root, "rev-parse", "--short", rev]).stdout.strip()
+    out = os.path.join(LIB_DIR, "alt", f"libnd_kernels_{sha}.so")
+    if os.path.exists(out):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    hipcc = _hipcc()
+    with tempfile.TemporaryDirectory() as td:
+        names = _run(["git", "-C", root, "ls-tree", "--name-only", rev, "nanodiloco_amd/csrc/"]).stdout.split()
+        srcs = []
+        for n in names:
+            if n.endswith((".hip", ".h")):
+                dst = os.path.join(td, os.path.basename(n))
+                with open(dst, "w") as f:
+                    f.write(_run(["git", "-C", root, "show", f"{rev}:{n}"]).stdout)
+                if n.endswith(".hip"):
+                    srcs.append(dst)
+        flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-I", td]
+
+        def comp(src):
+            o = src + ".o"
+            _run([hipcc] + flags + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", o])
+            return o
+
+        with cf.ThreadPoolExecutor(max_workers=jobs or min(8, os.cpu_count() or 4)) as ex:
+            objs = list(ex.map(comp, srcs))
+        # -Bsymbolic: the side library's references to its own kernel stubs must not bind to the
+        # identically named symbols of the main library already loaded RTLD_GLOBAL
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,-Bsymbolic", "-o", out] + objs)
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=0)
     ap.add_argument("--save-temps", action="store_true")
+    ap.add_argument("--rev", default=None, help="build the kernels of this git revision into _lib/alt/ (A/B)")
     a = ap.parse_args(argv)
+    if a.rev:
+        print(build_revision(a.rev, a.jobs))
+        return
     out = build(force=a.force, jobs=a.jobs, save_temps=a.save_temps, verbose=True)
     print(out)
 

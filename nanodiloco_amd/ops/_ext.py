@@ -57,6 +57,31 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+def load_library(path: str) -> "_StrictLib":
+    """Load another build of the kernel library side by side (RTLD_LOCAL) for in-process A/B."""
+    raw = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    _declare(raw)
+    return _StrictLib(raw)
+
+
+class using:
+    """``with _ext.using(other_lib): ...`` routes every op through `other_lib` (A/B benchmarking)."""
+
+    def __init__(self, other):
+        self.other = other
+
+    def __enter__(self):
+        global _lib
+        self.prev = lib()
+        _lib = self.other
+        return self.other
+
+    def __exit__(self, *exc):
+        global _lib
+        _lib = self.prev
+        return False
+
+
 def available() -> bool:
     try:
         lib()

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""In-process, interleaved A/B of two builds of the kernel library (cdna guide §5.4 rule 24:
+device-to-device and call-to-call variance on MI355X is several percent, so code versions are only
+compared inside one process, alternating).
+
+  python -m nanodiloco_amd.csrc.build --rev HEAD~1      # -> nanodiloco_amd/_lib/alt/libnd_kernels_<sha>.so
+  python scripts/ab_kernels.py --alt nanodiloco_amd/_lib/alt/libnd_kernels_<sha>.so --what attn
+
+--what attn : attention fwd+bwd on the Llama-150M micro-batch (per-kernel times via torch.profiler
+              are not needed: each op is timed with HIP events, min over rounds)
+--what step : one full forward+backward of Llama-150M (micro-batch 32 x 1024)
+--what wgrad: the wgrad GEMM shapes
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nanodiloco_amd import ops  # noqa: E402
+from nanodiloco_amd.ops import _ext  # noqa: E402
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def workloads(what):
+    from nanodiloco_amd.ops.attention import rope_cache
+    out = {}
+    if what == "attn":
+        B, T, nh, hd = 32, 1024, 16, 64
+        qkv = torch.randn(B * T, 3 * nh * hd, device="cuda").bfloat16()
+        cos, sin = rope_cache(T, hd, 10000.0, None, "cuda")
+        x = qkv.clone().requires_grad_(True)
+        o = ops.attention(x, cos, sin, B, T, nh, nh, hd)
+        do = torch.randn_like(o)
+        out["attn_fwd"] = lambda: ops.attention(x, cos, sin, B, T, nh, nh, hd)
+        out["attn_bwd"] = lambda: torch.autograd.grad(o, x, do, retain_graph=True)
+    elif what == "step":
+        from nanodiloco_amd.config import resolve_llama_config
+        from nanodiloco_amd.models import LlamaForCausalLM
+        cfg = resolve_llama_config("llama_150m.json")
+        m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16).init_weights(0)
+        ids = torch.randint(0, cfg.vocab_size, (32, 1024), device="cuda")
+
+        def step():
+            m(ids, labels=ids).loss.backward()
+        out["fwd_bwd"] = step
+    elif what == "wgrad":
+        from nanodiloco_amd.ops.gemm import wgrad
+        for name, (M, N) in {"qkv": (3072, 1024), "o": (1024, 1024), "gate_up": (5376, 1024),
+                             "down": (1024, 2688)}.items():
+            dy = torch.randn(32768, M, device="cuda").bfloat16()
+            xx = torch.randn(32768, N, device="cuda").bfloat16()
+            gw = torch.zeros(M, N, device="cuda")
+            out[name] = (lambda gw=gw, dy=dy, xx=xx: wgrad(gw, dy, xx))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--alt", required=True)
+    ap.add_argument("--what", default="attn", choices=["attn", "step", "wgrad"])
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    ops.set_backend("hip")
+    base = _ext.lib()
+    alt = _ext.load_library(a.alt)
+    wl = workloads(a.what)
+    res = {k: {"new": [], "alt": []} for k in wl}
+    for _ in range(a.rounds):
+        for k, fn in wl.items():
+            res[k]["new"].append(timed(fn, a.iters))
+            with _ext.using(alt):
+                res[k]["alt"].append(timed(fn, a.iters))
+    for k, r in res.items():
+        n, o = min(r["new"]), min(r["alt"])
+        print(f"{k:10s} working-tree {n:9.1f} us | alt {o:9.1f} us | speedup {o / n:5.3f}x", flush=True)
+    del base
+
+
+if __name__ == "__main__":
+    main()
