@@ -26,6 +26,7 @@
 // Causal: tiles past the diagonal are never loaded; fully masked (wave, tile) pairs are skipped;
 // the longest query / key blocks are dispatched first.
 #include "common.h"
+#include <cstdlib>
 #include <type_traits>
 
 using namespace nd;
@@ -265,8 +266,49 @@ __device__ __forceinline__ void store_T(bf16_t* out_row, f32x16* acc, float mul,
     }
 }
 
+namespace {
+__device__ __forceinline__ void adma_b128(const void* sbase, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void adma_b32(const void* sbase, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
+template <class T_>
+__device__ __forceinline__ uint32_t lds_addr(const T_* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) T_*)p);
+}
+}  // namespace
+
+// LDS-DMA of one ROWS x HD bf16 tile (row stride ld) into a soff<HD>-swizzled LDS tile by the 4 waves
+// of a workgroup: 1-KiB wave-instructions of 64/CPR rows, per-lane source offsets fixed per kernel.
+template <int HD, int ROWS>
+struct TileDma {
+  static constexpr int CPR = HD / 8, RPI = 64 / CPR, IPW = (ROWS / RPI) / 4;
+  uint32_t voff[IPW];
+  int wu;
+  __device__ __forceinline__ void init(int64_t ld) {
+    const int lane = threadIdx.x & 63;
+    wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int row = (wu + 4 * i) * RPI + lane / CPR, p = lane % CPR;
+      const int lch = (soff<HD>(row, p * 8) - row * HD) / 8;  // XOR swizzle: physical p holds logical lch
+      voff[i] = (uint32_t)(((int64_t)row * ld + lch * 8) * 2);
+    }
+  }
+  // rows row0.. of `base` (already offset to the tile's first row) -> LDS tile at byte address `lds`
+  __device__ __forceinline__ void issue(const bf16_t* base, uint32_t lds) const {
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) adma_b128(base, voff[i], lds + (uint32_t)((wu + 4 * i) * 1024));
+  }
+};
+
 // =============================================================================== forward
-template <int HD, bool ROPE>
+template <int HD, bool ROPE, bool DMA = false>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int nh, int nkv, int T,
@@ -300,20 +342,38 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
   const int ntiles = (min(T, qb * 128 + 128) + BN - 1) / BN;
   typename std::conditional<ROPE, StageRope<BN, HD>, Stage<BN, HD>>::type sk;
   Stage<BN, HD> sv;
-  // double-buffered tiles: compute(buf j&1) | regs hold tile j+1 | store -> buf (j+1)&1 | ONE barrier
-  load_tile<ROPE>(sk, Kb, ld, 0, T, cosT, sinT);
-  sv.load(Vb, ld, 0, T);
-  sk.store(Ks);
-  sv.store(Vs);
-  __syncthreads();
-  if (ntiles > 1) {
-    load_tile<ROPE>(sk, Kb, ld, BN, T, cosT, sinT);
-    sv.load(Vb, ld, BN, T);
+  TileDma<HD, BN> tdma;
+  const uint32_t ks_a = lds_addr(Ks), vs_a = lds_addr(Vs);
+  auto dma_issue = [&](int j) {
+    const uint32_t off = (uint32_t)((j & 1) * BN * HD * 2);
+    tdma.issue(Kb + (int64_t)j * BN * ld, ks_a + off);
+    tdma.issue(Vb + (int64_t)j * BN * ld, vs_a + off);
+  };
+  if constexpr (DMA) {
+    // double-buffered tiles: wait(tile j) + barrier | DMA tile j+1 -> buf (j+1)&1 | compute(buf j&1)
+    tdma.init(ld);
+    dma_issue(0);
+  } else {
+    // double-buffered tiles: compute(buf j&1) | regs hold tile j+1 | store -> buf (j+1)&1 | ONE barrier
+    load_tile<ROPE>(sk, Kb, ld, 0, T, cosT, sinT);
+    sv.load(Vb, ld, 0, T);
+    sk.store(Ks);
+    sv.store(Vs);
+    __syncthreads();
+    if (ntiles > 1) {
+      load_tile<ROPE>(sk, Kb, ld, BN, T, cosT, sinT);
+      sv.load(Vb, ld, BN, T);
+    }
   }
   for (int j = 0; j < ntiles; ++j) {
     const int k0 = j * BN;
     const bf16_t* Kt = Ks + (j & 1) * (BN * HD);
     const bf16_t* Vt = Vs + (j & 1) * (BN * HD);
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (j + 1 < ntiles) dma_issue(j + 1);
+    }
     if (k0 <= q0w + 31) {  // else: whole tile above this wave's diagonal (wave-uniform)
       // K row fragments issued up front (V^T transposing reads stay next to their MFMAs: holding
       // them too costs the third wave per SIMD)
@@ -371,14 +431,16 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
             oacc[o] = mfma32(tr_frag<HD>(Vt, kt * 32 + 16 * sidx, o * 32, g, i16), pf, oacc[o]);
         }
     }
-    if (j + 1 < ntiles) {
-      sk.store(Ks + ((j + 1) & 1) * (BN * HD));
-      sv.store(Vs + ((j + 1) & 1) * (BN * HD));
-    }
-    __syncthreads();
-    if (j + 2 < ntiles) {
-      load_tile<ROPE>(sk, Kb, ld, k0 + 2 * BN, T, cosT, sinT);
-      sv.load(Vb, ld, k0 + 2 * BN, T);
+    if constexpr (!DMA) {
+      if (j + 1 < ntiles) {
+        sk.store(Ks + ((j + 1) & 1) * (BN * HD));
+        sv.store(Vs + ((j + 1) & 1) * (BN * HD));
+      }
+      __syncthreads();
+      if (j + 2 < ntiles) {
+        load_tile<ROPE>(sk, Kb, ld, k0 + 2 * BN, T, cosT, sinT);
+        sv.load(Vb, ld, k0 + 2 * BN, T);
+      }
     }
   }
   const float lt = l + __shfl_xor(l, 32, 64);
@@ -420,7 +482,7 @@ __global__ void __launch_bounds__(256) attn_bwd_pre_kernel(const bf16_t* __restr
 }
 
 // dQ: per 128 queries of one (b, head), streaming 64-key K/V tiles up to the diagonal.
-template <int HD, bool ROPE, bool ROPE_OUT>
+template <int HD, bool ROPE, bool ROPE_OUT, bool DMA = false>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                              const bf16_t* __restrict__ V, const bf16_t* __restrict__ dO,
                                                              const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -461,19 +523,36 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
   const int ntiles = (min(T, qb * 128 + 128) + BN - 1) / BN;
   typename std::conditional<ROPE, StageRope<BN, HD>, Stage<BN, HD>>::type sk;
   Stage<BN, HD> sv;
-  load_tile<ROPE>(sk, Kb, ld, 0, T, cosT, sinT);
-  sv.load(Vb, ld, 0, T);
-  sk.store(Ks);
-  sv.store(Vs);
-  __syncthreads();
-  if (ntiles > 1) {
-    load_tile<ROPE>(sk, Kb, ld, BN, T, cosT, sinT);
-    sv.load(Vb, ld, BN, T);
+  TileDma<HD, BN> tdma;
+  const uint32_t ks_a = lds_addr(Ks), vs_a = lds_addr(Vs);
+  auto dma_issue = [&](int j) {
+    const uint32_t off = (uint32_t)((j & 1) * BN * HD * 2);
+    tdma.issue(Kb + (int64_t)j * BN * ld, ks_a + off);
+    tdma.issue(Vb + (int64_t)j * BN * ld, vs_a + off);
+  };
+  if constexpr (DMA) {
+    tdma.init(ld);
+    dma_issue(0);
+  } else {
+    load_tile<ROPE>(sk, Kb, ld, 0, T, cosT, sinT);
+    sv.load(Vb, ld, 0, T);
+    sk.store(Ks);
+    sv.store(Vs);
+    __syncthreads();
+    if (ntiles > 1) {
+      load_tile<ROPE>(sk, Kb, ld, BN, T, cosT, sinT);
+      sv.load(Vb, ld, BN, T);
+    }
   }
   for (int j = 0; j < ntiles; ++j) {
     const int k0 = j * BN;
     const bf16_t* Kt = Ks + (j & 1) * (BN * HD);
     const bf16_t* Vt = Vs + (j & 1) * (BN * HD);
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (j + 1 < ntiles) dma_issue(j + 1);
+    }
     if (k0 <= q0w + 31) {
       const bool diag = (k0 + BN - 1 > q0w) || (k0 + BN > T) || (qi >= T);
 #pragma unroll
@@ -515,14 +594,16 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
         }
       }
     }
-    if (j + 1 < ntiles) {
-      sk.store(Ks + ((j + 1) & 1) * (BN * HD));
-      sv.store(Vs + ((j + 1) & 1) * (BN * HD));
-    }
-    __syncthreads();
-    if (j + 2 < ntiles) {
-      load_tile<ROPE>(sk, Kb, ld, k0 + 2 * BN, T, cosT, sinT);
-      sv.load(Vb, ld, k0 + 2 * BN, T);
+    if constexpr (!DMA) {
+      if (j + 1 < ntiles) {
+        sk.store(Ks + ((j + 1) & 1) * (BN * HD));
+        sv.store(Vs + ((j + 1) & 1) * (BN * HD));
+      }
+      __syncthreads();
+      if (j + 2 < ntiles) {
+        load_tile<ROPE>(sk, Kb, ld, k0 + 2 * BN, T, cosT, sinT);
+        sv.load(Vb, ld, k0 + 2 * BN, T);
+      }
     }
   }
   if (qi < T)
@@ -688,6 +769,9 @@ static int fwd_launch(const void* q, const void* k, const void* v, void* o, floa
   if (cosT)
     hipLaunchKernelGGL((attn_fwd_kernel<HD, true>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+  else if (T % 64 == 0 && !(getenv("ND_ATTN_FWD") && getenv("ND_ATTN_FWD")[0] == 'r'))
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, false, true>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k,
+                       (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
   else
     hipLaunchKernelGGL((attn_fwd_kernel<HD, false>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
@@ -721,45 +805,230 @@ ND_API int nd_attn_bwd_pre(const void* o, const void* dout, float* delta, int B,
   ND_LAUNCH_CHECK();
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// dK, dV with LDS-DMA staging (T % 64 == 0, q/k already rotated): the Q / dO tiles and the row
+// statistics of query tile it+1 move global -> LDS with global_load_lds (no VGPR round trip, no
+// ds_write, no staging registers) while tile it is computed.  Row statistics come pre-negated
+// (-LSE/c, -delta: attn_neg_stats_kernel) so they seed the S / dP accumulators directly.
+
+__global__ void __launch_bounds__(256) attn_neg_stats_kernel(const float* __restrict__ lse, const float* __restrict__ delta,
+                                                             float* __restrict__ nl, float* __restrict__ nd, int64_t n,
+                                                             float inv_c) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    nl[i] = -lse[i] * inv_c;
+    nd[i] = -delta[i];
+  }
+}
+
+template <int HD, bool ROPE_OUT>
+__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const bf16_t* __restrict__ dO, const float* __restrict__ NL, const float* __restrict__ ND, bf16_t* __restrict__ dK,
+    bf16_t* __restrict__ dV, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
+    const float* __restrict__ cosT, const float* __restrict__ sinT) {
+  constexpr int BQ = 64, NT = HD / 16, NO = HD / 32;
+  constexpr int CPR = HD / 8;              // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;            // rows per 1-KiB DMA wave-instruction
+  constexpr int IPW = (BQ / RPI) / 4;      // DMA instructions per wave per operand tile
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[2 * BQ * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[2 * BQ * HD];
+  __shared__ __attribute__((aligned(16))) float lse_s[2 * BQ];
+  __shared__ __attribute__((aligned(16))) float del_s[2 * BQ];
+
+  const int bk_count = B * nkv, rep = nh / nkv;
+  const int kb = (int)(blockIdx.x / bk_count);
+  const int bk = blockIdx.x % bk_count;
+  const int b = bk / nkv, kvh = bk % nkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int kw0 = kb * 128 + w * 32, key = kw0 + c32;
+  const float c = scale * LOG2E;
+  const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
+  const bf16_t* Vb = V + (int64_t)b * T * ld + (int64_t)kvh * HD;
+
+  bf16x8 kf[NT], vf[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    kf[t] = key < T ? load16(Kb + (int64_t)key * ld + 16 * t + 8 * h) : zero8();
+    vf[t] = key < T ? load16(Vb + (int64_t)key * ld + 16 * t + 8 * h) : zero8();
+  }
+  f32x16 dk[NO], dv[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) { dk[o] = f32x16{}; dv[o] = f32x16{}; }
+
+  // per-lane DMA source offsets (constant over tiles): physical chunk p of row r carries logical
+  // chunk p ^ key(r) of the soff<HD> swizzle (an XOR involution)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  uint32_t vq[IPW], vd[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int row = (wu + 4 * i) * RPI + lane / CPR, p = lane % CPR;
+    const int lch = (soff<HD>(row, p * 8) - row * HD) / 8;  // soff maps logical -> physical; XOR: same map back
+    vq[i] = (uint32_t)(((int64_t)row * ld + lch * 8) * 2);
+    vd[i] = (uint32_t)(((int64_t)row * ldo + lch * 8) * 2);
+  }
+  const uint32_t qs_a = lds_addr(Qs), do_a = lds_addr(dOs), ls_a = lds_addr(lse_s), ds_a = lds_addr(del_s);
+
+  const int qstart = (kb * 128) / BQ * BQ;
+  const int ntq = (T - qstart + BQ - 1) / BQ;
+  const int nit = ntq * rep;
+  auto issue = [&](int it) {
+    const int head = kvh * rep + it / ntq;
+    const int q0 = qstart + (it % ntq) * BQ;
+    const int buf = it & 1;
+    const bf16_t* sq = Q + ((int64_t)b * T + q0) * ld + (int64_t)head * HD;
+    const bf16_t* sd = dO + ((int64_t)b * T + q0) * ldo + (int64_t)head * HD;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const uint32_t off = (uint32_t)(buf * BQ * HD * 2 + (wu + 4 * i) * 1024);
+      adma_b128(sq, vq[i], qs_a + off);
+      adma_b128(sd, vd[i], do_a + off);
+    }
+    if (wu == 0) {
+      const int64_t rs = ((int64_t)b * nh + head) * T + q0;
+      adma_b32(NL + rs, (uint32_t)(lane * 4), ls_a + buf * BQ * 4);
+      adma_b32(ND + rs, (uint32_t)(lane * 4), ds_a + buf * BQ * 4);
+    }
+  };
+  issue(0);
+  for (int it = 0; it < nit; ++it) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of tile it has landed
+    __syncthreads();                                  // everyone's; and tile it-1's buffer is free
+    if (it + 1 < nit) issue(it + 1);
+    const int q0 = qstart + (it % ntq) * BQ;
+    const int buf = it & 1;
+    const bf16_t* Qt = Qs + buf * (BQ * HD);
+    const bf16_t* dOt = dOs + buf * (BQ * HD);
+    const float* lt = lse_s + buf * BQ;
+    const float* dt = del_s + buf * BQ;
+#pragma unroll
+    for (int qs = 0; qs < BQ / 32; ++qs) {
+      const int qsub = q0 + qs * 32;
+      if (kw0 > qsub + 31 || kw0 >= T) continue;  // wave-uniform: no query >= any of our keys
+      // All LDS fragments of this step are issued up front (row reads for S / dP, transposing reads
+      // for dV / dK) so their latency hides behind the MFMA chains and the softmax VALU instead of
+      // being exposed one s_waitcnt at a time.
+      bf16x8 qa[NT], da[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        qa[t] = row_frag<HD>(Qt, qs * 32 + c32, t, h);
+        da[t] = row_frag<HD>(dOt, qs * 32 + c32, t, h);
+      }
+      f32x16 s, dp;  // seeded with -LSE / c and -delta of each query row
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int qr = qs * 32 + 8 * r4 + 4 * h;
+        const float4 l4 = *reinterpret_cast<const float4*>(lt + qr);
+        const float4 d4 = *reinterpret_cast<const float4*>(dt + qr);
+        s[4 * r4 + 0] = l4.x; s[4 * r4 + 1] = l4.y; s[4 * r4 + 2] = l4.z; s[4 * r4 + 3] = l4.w;
+        dp[4 * r4 + 0] = d4.x; dp[4 * r4 + 1] = d4.y; dp[4 * r4 + 2] = d4.z; dp[4 * r4 + 3] = d4.w;
+      }
+      bf16x8 tdo[2][NO], tq[2][NO];
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx)
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+          tdo[sidx][o] = tr_frag<HD>(dOt, qs * 32 + 16 * sidx, o * 32, g, i16);
+          tq[sidx][o] = tr_frag<HD>(Qt, qs * 32 + 16 * sidx, o * 32, g, i16);
+        }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        s = mfma32(qa[t], kf[t], s);
+        dp = mfma32(da[t], vf[t], dp);
+      }
+      const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T);
+      if (!diag) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(s[r] * c);
+          s[r] = p;
+          dp[r] = p * dp[r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qq = qsub + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float p = (key <= qq && qq < T && key < T) ? fexp2(s[r] * c) : 0.f;
+          s[r] = p;
+          dp[r] = p * dp[r];
+        }
+      }
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx) {
+        const bf16x8 pf = pack_frag(s, sidx);
+        const bf16x8 dsf = pack_frag(dp, sidx);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+          dv[o] = mfma32(tdo[sidx][o], pf, dv[o]);
+          dk[o] = mfma32(tq[sidx][o], dsf, dk[o]);
+        }
+      }
+    }
+  }
+  if (key < T) {
+    store_T<HD>(dK + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dk, scale, h, ROPE_OUT ? cosT : nullptr, sinT, key);
+    store_T<HD>(dV + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dv, 1.f, h, nullptr, nullptr, 0);
+  }
+}
+
 template <int HD, bool ROPE, bool ROPE_OUT>
 static void bwd_launch_t(const void* q, const void* k, const void* v, const void* dout, const float* lse,
-                         const float* delta, void* dq, void* dk, void* dv, int B, int nh, int nkv, int T, int64_t ld,
-                         int64_t ldo, const float* cosT, const float* sinT, float scale, hipStream_t s) {
+                         const float* delta, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T,
+                         int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, hipStream_t s) {
   const int nb = (T + 127) / 128;
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, ROPE, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s, (const bf16_t*)q,
-                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, B,
-                     nh, nkv, T, ld, ldo, scale, cosT, sinT);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT>), dim3(nb * B * nh), dim3(256), 0, s, (const bf16_t*)q,
-                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, nh, nkv, T,
-                     ld, ldo, scale, cosT, sinT);
+  const char* ev = getenv("ND_ATTN_DKDV");
+  const bool dma = !ROPE && ws != nullptr && T % 64 == 0 && !(ev && ev[0] == 'r');
+  if (dma) {
+    const int64_t n = (int64_t)B * nh * T;
+    float *nl = ws, *nd = ws + n;
+    hipLaunchKernelGGL(attn_neg_stats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lse, delta, nl, nd, n,
+                       1.f / (scale * LOG2E));
+    hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
+                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, ROPE, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,
+                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+  }
+  if (dma)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT, !ROPE>), dim3(nb * B * nh), dim3(256), 0, s,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,
+                       (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+  else
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT>), dim3(nb * B * nh), dim3(256), 0, s, (const bf16_t*)q,
+                       (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, nh, nkv,
+                       T, ld, ldo, scale, cosT, sinT);
 }
 
 // rope_mode 0: no RoPE; 1: q/k are RAW projections -- rotated on load, dq/dk un-rotated on store;
 // 2: q/k were rotated in place before the forward -- only the dq/dk un-rotation (store epilogue).
 template <int HD>
 static int bwd_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse, const float* delta,
-                      void* dq, void* dk, void* dv, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo,
+                      void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo,
                       const float* cosT, const float* sinT, float scale, int rope_mode, hipStream_t s) {
   if (rope_mode == 1)
-    bwd_launch_t<HD, true, true>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
+    bwd_launch_t<HD, true, true>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
   else if (rope_mode == 2)
-    bwd_launch_t<HD, false, true>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
+    bwd_launch_t<HD, false, true>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
   else
-    bwd_launch_t<HD, false, false>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
+    bwd_launch_t<HD, false, false>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
   ND_LAUNCH_CHECK();
 }
 
 // dq/dk/dv may point into one packed dqkv buffer (row stride ld).
 ND_API int nd_attn_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
-                       const float* delta, void* dq, void* dk, void* dv, float* /*unused*/, int B, int nh, int nkv,
+                       const float* delta, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv,
                        int T, int hd, int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale,
                        int rope_mode, hipStream_t s) {
   if (nh % nkv || (ld % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
   if (rope_mode && !(cosT && sinT)) return (int)hipErrorInvalidValue;
   switch (hd) {
-    case 32: return bwd_launch<32>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
-    case 64: return bwd_launch<64>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
-    case 128: return bwd_launch<128>(q, k, v, dout, lse, delta, dq, dk, dv, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
+    case 32: return bwd_launch<32>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
+    case 64: return bwd_launch<64>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
+    case 128: return bwd_launch<128>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
     default: return (int)hipErrorInvalidValue;
   }
 }

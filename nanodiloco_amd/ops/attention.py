@@ -78,8 +78,9 @@ class FlashAttnFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         k, v = qkv[:, nh * hd:], qkv[:, (nh + nkv) * hd:]
         dk, dv = dqkv[:, nh * hd:], dqkv[:, (nh + nkv) * hd:]
+        ws = torch.empty(2, B, nh, T, dtype=torch.float32, device=dev)  # -LSE/c, -delta for the dK/dV kernel
         _ext.check(L.nd_attn_bwd(_ext.ptr(qkv), _ext.ptr(k), _ext.ptr(v), _ext.ptr(do), _ext.ptr(lse), _ext.ptr(delta),
-                                 _ext.ptr(dqkv), _ext.ptr(dk), _ext.ptr(dv), 0,
+                                 _ext.ptr(dqkv), _ext.ptr(dk), _ext.ptr(dv), _ext.ptr(ws),
                                  B, nh, nkv, T, hd, ld, nh * hd, _ext.ptr(cos), _ext.ptr(sin), float(hd ** -0.5), 2,
                                  _ext.stream_ptr(dev)), "nd_attn_bwd")
         return dqkv, None, None, None, None, None, None, None
