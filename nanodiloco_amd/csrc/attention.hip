@@ -822,13 +822,13 @@ __global__ void __launch_bounds__(256) attn_neg_stats_kernel(const float* __rest
   }
 }
 
-template <int HD, bool ROPE_OUT>
+template <int HD, bool ROPE_OUT, int BQ = 64>
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ NL, const float* __restrict__ ND, bf16_t* __restrict__ dK,
     bf16_t* __restrict__ dV, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
     const float* __restrict__ cosT, const float* __restrict__ sinT) {
-  constexpr int BQ = 64, NT = HD / 16, NO = HD / 32;
+  constexpr int NT = HD / 16, NO = HD / 32;
   constexpr int CPR = HD / 8;              // 16-B chunks per row
   constexpr int RPI = 64 / CPR;            // rows per 1-KiB DMA wave-instruction
   constexpr int IPW = (BQ / RPI) / 4;      // DMA instructions per wave per operand tile
@@ -886,10 +886,10 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
       adma_b128(sq, vq[i], qs_a + off);
       adma_b128(sd, vd[i], do_a + off);
     }
-    if (wu == 0) {
-      const int64_t rs = ((int64_t)b * nh + head) * T + q0;
-      adma_b32(NL + rs, (uint32_t)(lane * 4), ls_a + buf * BQ * 4);
-      adma_b32(ND + rs, (uint32_t)(lane * 4), ds_a + buf * BQ * 4);
+    if (wu < BQ / 64) {  // one 64-float wave-instruction per 64 rows
+      const int64_t rs = ((int64_t)b * nh + head) * T + q0 + wu * 64;
+      adma_b32(NL + rs, (uint32_t)(lane * 4), ls_a + (buf * BQ + wu * 64) * 4);
+      adma_b32(ND + rs, (uint32_t)(lane * 4), ds_a + (buf * BQ + wu * 64) * 4);
     }
   };
   issue(0);
@@ -985,9 +985,15 @@ static void bwd_launch_t(const void* q, const void* k, const void* v, const void
     float *nl = ws, *nd = ws + n;
     hipLaunchKernelGGL(attn_neg_stats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lse, delta, nl, nd, n,
                        1.f / (scale * LOG2E));
-    hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
-                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
-                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+    const char* bq = getenv("ND_DKDV_BQ");  // "64": 64-query tiles (A/B); default 128 when T allows
+    if (!(bq && bq[0] == '6') && T % 128 == 0)
+      hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128>), dim3(nb * B * nkv), dim3(256), 0, s,
+                         (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
+                         (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+    else
+      hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
+                         (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
+                         (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
   } else {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, ROPE, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,
