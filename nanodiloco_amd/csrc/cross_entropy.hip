@@ -9,6 +9,7 @@
 // scale = loss_scale / n_valid lives in device memory (no host sync).  Rows whose target is
 // ignore_index contribute 0 loss and 0 gradient.  Larger vocabularies use the two-pass variant.
 #include "common.h"
+#include <cstdlib>
 
 using namespace nd;
 
@@ -82,6 +83,88 @@ __global__ void __launch_bounds__(256) ce_reg_kernel(void* __restrict__ logits, 
   if (threadIdx.x == 0 && valid) atomicAdd(loss_sum, lse - picked);
 }
 
+
+// bf16 rows, packed: the row stays in registers as raw bf16 pairs (CH x 4 VGPRs instead of CH x 8
+// fp32), so more waves fit per SIMD to keep the 64-KiB row loads in flight; scores are handled in
+// the log2 domain (one FMA + v_exp_f32 per element and pass); the target column is fixed up once by
+// the thread that owns it instead of a compare per element.
+template <int CH>
+__global__ void __launch_bounds__(256) ce_bf16_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
+                                                      float* __restrict__ loss_sum, const float* __restrict__ scale_p,
+                                                      int V, int ignore, float* __restrict__ lse_out) {
+  constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+  __shared__ float red[8];
+  const int64_t row = blockIdx.x;
+  bf16_t* rp = logits + row * (int64_t)V;
+  const int tgt = (int)targets[row];
+  const bool valid = tgt != ignore;
+  uint4 x[CH];
+  float m = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 256 + threadIdx.x) * 8;
+    if (col < V) {
+      x[c] = *reinterpret_cast<const uint4*>(rp + col);
+      const uint32_t u[4] = {x[c].x, x[c].y, x[c].z, x[c].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m = fmaxf(m, fmaxf(lo_bf(u[j]), hi_bf(u[j])));
+    }
+  }
+  m = block_max<256>(m, red);
+  const float m2 = m * L2E;
+  // opaque to the optimiser: stops it from keeping the unpacked fp32 copies alive across passes
+#pragma unroll
+  for (int c = 0; c < CH; ++c) asm volatile("" : "+v"(x[c].x), "+v"(x[c].y), "+v"(x[c].z), "+v"(x[c].w));
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 256 + threadIdx.x) * 8;
+    if (col < V) {
+      const uint32_t u[4] = {x[c].x, x[c].y, x[c].z, x[c].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        s += __builtin_amdgcn_exp2f(fmaf(lo_bf(u[j]), L2E, -m2)) + __builtin_amdgcn_exp2f(fmaf(hi_bf(u[j]), L2E, -m2));
+    }
+  }
+  __syncthreads();
+  s = block_sum<256>(s, red);
+  const float lse2 = m2 + __log2f(s);  // log2-domain logsumexp
+#pragma unroll
+  for (int c = 0; c < CH; ++c) asm volatile("" : "+v"(x[c].x), "+v"(x[c].y), "+v"(x[c].z), "+v"(x[c].w));
+  const float sc = valid ? scale_p[0] : 0.f;
+  float picked = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 256 + threadIdx.x) * 8;
+    if (col < V) {
+      const uint32_t u[4] = {x[c].x, x[c].y, x[c].z, x[c].w};
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[2 * j] = __builtin_amdgcn_exp2f(fmaf(lo_bf(u[j]), L2E, -lse2)) * sc;
+        o[2 * j + 1] = __builtin_amdgcn_exp2f(fmaf(hi_bf(u[j]), L2E, -lse2)) * sc;
+      }
+      const unsigned d = (unsigned)(tgt - col);
+      if (d < 8u) {  // this thread owns the target column
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if ((unsigned)j == d) {
+            picked = (j & 1) ? hi_bf(u[j >> 1]) : lo_bf(u[j >> 1]);
+            o[j] -= sc;
+          }
+      }
+      uint4 w;
+      w.x = pack2(o[0], o[1]); w.y = pack2(o[2], o[3]); w.z = pack2(o[4], o[5]); w.w = pack2(o[6], o[7]);
+      *reinterpret_cast<uint4*>(rp + col) = w;
+    }
+  }
+  const float lse = lse2 * LN2;
+  if (threadIdx.x == 0 && lse_out) lse_out[row] = lse;
+  __syncthreads();
+  picked = block_sum<256>(picked, red);
+  if (threadIdx.x == 0 && valid) atomicAdd(loss_sum, lse - picked);
+}
+
 // Generic two-pass variant (any V, scalar accesses): online max/sum, then gradient write.
 template <int DT>
 __global__ void __launch_bounds__(256) ce_generic_kernel(void* __restrict__ logits, const int64_t* __restrict__ targets,
@@ -134,7 +217,10 @@ ND_API int nd_ce_fwd_bwd(void* logits, int dt, const int64_t* targets, float* lo
       if (dt == BF16) hipLaunchKernelGGL((ce_reg_kernel<BF16, 4>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out);
       else hipLaunchKernelGGL((ce_reg_kernel<F32, 4>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out);
     } else {
-      if (dt == BF16) hipLaunchKernelGGL((ce_reg_kernel<BF16, 16>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out);
+      const char* ev = getenv("ND_CE");
+      if (dt == BF16 && !(ev && ev[0] == 'r'))
+        hipLaunchKernelGGL((ce_bf16_kernel<16>), g, b, 0, s, (bf16_t*)logits, targets, loss_sum, scale, V, ignore, lse_out);
+      else if (dt == BF16) hipLaunchKernelGGL((ce_reg_kernel<BF16, 16>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out);
       else hipLaunchKernelGGL((ce_reg_kernel<F32, 16>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out);
     }
   } else {

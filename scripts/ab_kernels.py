@@ -56,6 +56,17 @@ def workloads(what):
         def step():
             m(ids, labels=ids).loss.backward()
         out["fwd_bwd"] = step
+    elif what == "ce":
+        V, n = 32000, 16384
+        logits = torch.randn(n, V, device="cuda").bfloat16()
+        tgt = torch.randint(0, V, (n,), device="cuda")
+        loss = torch.zeros(1, device="cuda")
+        sc = torch.ones(1, device="cuda")
+
+        def ce():
+            _ext.check(_ext.lib().nd_ce_fwd_bwd(logits.data_ptr(), 1, tgt.data_ptr(), loss.data_ptr(), sc.data_ptr(),
+                                                n, V, -100, 0, 0, 0.0, _ext.stream_ptr()), "ce")
+        out["ce_16k"] = ce
     elif what == "wgrad":
         from nanodiloco_amd.ops.gemm import wgrad
         for name, (M, N) in {"qkv": (3072, 1024), "o": (1024, 1024), "gate_up": (5376, 1024),
@@ -70,7 +81,7 @@ def workloads(what):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--alt", required=True)
-    ap.add_argument("--what", default="attn", choices=["attn", "step", "wgrad"])
+    ap.add_argument("--what", default="attn", choices=["attn", "step", "wgrad", "ce"])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
