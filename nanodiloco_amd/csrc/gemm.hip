@@ -147,6 +147,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_kernel(const bf16_t* __restric
 }
 
 
+
 // C[M, N] = A[M, K] . B[N, K]^T (bf16 in / bf16 out, fp32 accumulate).  K % 64 == 0, N % 4 == 0,
 // lda / ldb % 8 == 0, ldc % 4 == 0.
 ND_API int nd_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb,
