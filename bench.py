@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="llama_150m.json")
     ap.add_argument("--batch-size", type=int, default=256, help="sequences per worker per inner step (reference)")
-    ap.add_argument("--micro-batch", type=int, default=32, help="sequences per forward/backward")
+    ap.add_argument("--micro-batch", type=int, default=64,
+                    help="sequences per forward/backward (64: best of 16/32/64/128/256 on MI355X, same global batch)")
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--inner-steps", type=int, default=100)
     ap.add_argument("--inner-dp", type=int, default=1)
