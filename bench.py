@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=128.0)
     ap.add_argument("--overlap-outer", action="store_true")
     ap.add_argument("--no-tuned-gemm", action="store_true", help="library-default GEMM algorithms (A/B)")
+    ap.add_argument("--hip-graph", action="store_true",
+                    help="capture the micro-batch forward+backward in a HIP graph (launch-bound small models)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
     ap.add_argument("--fp8-wgrad", action="store_true", help="with --fp8: weight-gradient GEMM in fp8 too")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
@@ -91,15 +93,26 @@ def main():
     model.train()
     state = {"step": 0}
 
+    graphed = None
+    if a.hip_graph:
+        if env.inner_dp > 1:
+            raise SystemExit("--hip-graph needs --inner-dp 1")
+        from nanodiloco_amd.utils.graphs import GraphedMicroStep
+        graphed = GraphedMicroStep(model)
+
     def inner_step():
         loss = None
         for m in range(accum):
             b = next(data)
             if m == accum - 1:
                 isync.arm()
-            out = model(b["input_ids"], labels=b["labels"], loss_scale=loss_scale)
-            out.loss.backward()
-            loss = out.loss.detach() if loss is None else loss + out.loss.detach()
+            if graphed is not None:
+                l_m = graphed(b["input_ids"], b["labels"], loss_scale)
+            else:
+                out = model(b["input_ids"], labels=b["labels"], loss_scale=loss_scale)
+                out.loss.backward()
+                l_m = out.loss.detach()
+            loss = l_m.clone() if loss is None else loss + l_m
         isync.finish()
         dl.inner_step()
         state["step"] += 1

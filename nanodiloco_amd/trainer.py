@@ -66,6 +66,7 @@ class TrainArgs:
     activation_checkpointing: bool = False
     fp8: bool = False              # fp8 e4m3/e5m2 decoder projections (GPU, bf16 compute)
     tuned_gemm: bool = True        # load the pre-tuned hipBLASLt algorithm table (ops/tuned_gemm.py)
+    hip_graph: bool = False        # capture the micro-batch fwd+bwd in a HIP graph (utils/graphs.py)
     checkpoint_dir: Optional[str] = None
     checkpoint_every: int = 0      # in outer steps (0 = only at the end when checkpoint_dir is set)
     stop_at_step: int = 0          # stop early (simulated preemption) after this inner step; 0 = run to total
@@ -149,6 +150,12 @@ class Trainer:
                     self.data.load_state_dict(st["data_state"])
                 except Exception:
                     pass
+        self.graphed = None
+        if a.hip_graph:
+            if e.device.type != "cuda" or e.inner_dp > 1 or self.model.fp8 is not None:
+                raise ValueError("--hip-graph needs a GPU, --inner-dp 1 and no --fp8")
+            from .utils.graphs import GraphedMicroStep
+            self.graphed = GraphedMicroStep(self.model)
         self.run_name = create_run_name("nanodiloco", self.run_config, is_debug=False)
         self.timer = PhaseTimer(a.phase_timing)
         self.sink = make_sink(e.rank, a.project, self.run_name, {**self.run_config, **dataclasses.asdict(a)},
@@ -163,9 +170,12 @@ class Trainer:
                 batch = next(self.data)
                 if micro == self.grad_accum - 1:
                     self.inner_sync.arm()
-                out = self.model(batch["input_ids"], labels=batch["labels"], loss_scale=self.loss_scale)
-                out.loss.backward()
-                l = out.loss.detach()
+                if self.graphed is not None:
+                    l = self.graphed(batch["input_ids"], batch["labels"], self.loss_scale).clone()
+                else:
+                    out = self.model(batch["input_ids"], labels=batch["labels"], loss_scale=self.loss_scale)
+                    out.loss.backward()
+                    l = out.loss.detach()
                 loss_sum = l if loss_sum is None else loss_sum + l
         with self.timer.phase("inner_opt"):
             self.inner_sync.finish()
