@@ -63,6 +63,11 @@ def parse():
     ap.add_argument("--no-tuned-gemm", action="store_true", help="library-default GEMM algorithms (A/B)")
     ap.add_argument("--hip-graph", action="store_true",
                     help="capture the micro-batch forward+backward in a HIP graph (launch-bound small models)")
+    ap.add_argument("--wgrad-overlap", type=int, default=0, choices=[0, 1, 2],
+                    help="issue weight-gradient GEMMs on a side HIP stream (overlaps the dgrad chain); off by "
+                         "default: beside hipBLASLt's stream-K GEMMs it stalls (docs/DESIGN.md)")
+    ap.add_argument("--dgrad-t", type=int, default=1, choices=[0, 1],
+                    help="input-gradient GEMMs on transposed weight copies (K-contiguous NT layout)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
     ap.add_argument("--fp8-wgrad", action="store_true", help="with --fp8: weight-gradient GEMM in fp8 too")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
@@ -72,6 +77,8 @@ def parse():
 def main():
     a = parse()
     ops.set_backend(a.ops)
+    ops.set_wgrad_overlap(a.wgrad_overlap)
+    ops.set_dgrad_transposed(bool(a.dgrad_t))
     env = init_distributed(a.backend, a.inner_dp)
     if env.world_size != a.gpus and env.rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
@@ -189,6 +196,8 @@ def main():
             "model_tflops_per_gpu": round(mfu_flops / 1e12, 2),
             "final_loss": round(final_loss, 4),
             "tuned_gemm": enable_tuned_gemms(env.device) if env.device.type == "cuda" and not a.no_tuned_gemm else False,
+            "wgrad_overlap": ops.wgrad_overlap_enabled(),
+            "dgrad_transposed": ops.dgrad_transposed_enabled(),
             "ops": ops.get_backend() if a.ops != "auto" else ("hip" if env.device.type == "cuda" else "torch"),
         }
         print(json.dumps(out), flush=True)

@@ -198,3 +198,53 @@ ND_API int nd_rmsnorm_bwd(const void* dy, int dydt, const float* h, const float*
     default: return bwd_dispatch<8>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
   }
 }
+
+// out[c] += sum_r part[r][c]: the RMSNorm weight-gradient partials (one row per backward block)
+// summed into the flat fp32 grad buffer in a fixed order (deterministic).  Latency-bound (a few MB):
+// one workgroup per 64 columns, 16 row groups x 16 float4 column quads, 8 independent float4 loads
+// in flight per thread, row groups combined through LDS.
+__global__ void __launch_bounds__(256) colsum_add_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                         int rows, int cols) {
+  __shared__ float4 red[16][17];
+  const int q = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + q * 4;
+  const bool ok = c < cols;  // cols % 4 == 0 (host check)
+  float4 acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    int r = rg;
+    for (; r + 7 * 16 < rows; r += 8 * 16) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)(r + u * 16) * cols + c);
+        acc[u].x += v.x; acc[u].y += v.y; acc[u].z += v.z; acc[u].w += v.w;
+      }
+    }
+    for (; r < rows; r += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)r * cols + c);
+      acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
+    }
+  }
+  float4 t = acc[0];
+#pragma unroll
+  for (int u = 1; u < 8; ++u) { t.x += acc[u].x; t.y += acc[u].y; t.z += acc[u].z; t.w += acc[u].w; }
+  red[rg][q] = t;
+  __syncthreads();
+  if (rg == 0 && ok) {
+    float4 s = red[0][q];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) { s.x += red[g][q].x; s.y += red[g][q].y; s.z += red[g][q].z; s.w += red[g][q].w; }
+    float4* o = reinterpret_cast<float4*>(out + c);
+    float4 v = *o;
+    v.x += s.x; v.y += s.y; v.z += s.z; v.w += s.w;
+    *o = v;
+  }
+}
+
+ND_API int nd_colsum_add(const float* part, float* out, int rows, int cols, hipStream_t s) {
+  if (rows <= 0 || cols <= 0 || cols % 4 || ((uintptr_t)part & 15) || ((uintptr_t)out & 15))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(colsum_add_kernel, dim3((unsigned)((cols + 63) / 64)), dim3(256), 0, s, part, out, rows, cols);
+  ND_LAUNCH_CHECK();
+}

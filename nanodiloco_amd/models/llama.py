@@ -46,6 +46,7 @@ class _GradHook(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        ops.join_wgrad()  # the layer's weight gradients may still be in flight on the side stream
         ctx.fn(ctx.idx)
         return g, None, None
 
@@ -68,6 +69,9 @@ class LlamaForCausalLM:
         self._qkv_names = [g for g in groups[0::2]]
         self._gu_names = [g for g in groups[1::2]]
         self.layer_hook: Optional[Callable[[int], None]] = None
+        # W^T copies for the input-gradient GEMMs (ops/linear.py), refreshed lazily whenever the
+        # store's weight version moves: key -> [W^T buffer, version it holds, W view]
+        self._wt_cache = {}
         self.training = True
         self.fp8 = None
         if fp8:
@@ -134,10 +138,33 @@ class LlamaForCausalLM:
         return self.store.fused_view(which, names)
 
     # ------------------------------------------------------------------ forward
+    def _wt(self, key, w):
+        """W^T (contiguous) for the dgrad GEMM, or None when the plain layout is used."""
+        if not (self.training and w.is_cuda and w.dtype == torch.bfloat16 and ops.dgrad_transposed_enabled()):
+            return None
+        e = self._wt_cache.get(key)
+        if e is None:
+            e = [torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device), -1, w]
+            self._wt_cache[key] = e
+        if e[1] != self.store.version:
+            ops.transpose_into(e[0], w)
+            e[1] = self.store.version
+        return e[0]
+
+    def refresh_transposed(self):
+        """Bring every cached W^T up to the current weights (eagerly, e.g. before a HIP-graph
+        replay, whose captured GEMMs read these buffers but never re-run the version check)."""
+        if not ops.dgrad_transposed_enabled():
+            return
+        for key, e in self._wt_cache.items():
+            if e[1] != self.store.version:
+                ops.transpose_into(e[0], e[2])
+                e[1] = self.store.version
+
     def _linear(self, key, x, w, gw):
         if self.fp8 is not None:
             return self.fp8(key, x, w, gw, self.store.version)
-        return ops.linear(x, w, gw)
+        return ops.linear(x, w, gw, self._wt(key, w))
 
     def _layer(self, i, h, y, cos, sin, B, T, next_norm):
         c = self.config
@@ -192,7 +219,9 @@ class LlamaForCausalLM:
         if labels is not None or targets is not None:
             if targets is None:
                 targets = ops.reference.shift_labels(labels, ops.IGNORE_INDEX)
-            out.loss = ops.lm_head_ce(y, self._w(lm), self._g(lm), targets.reshape(-1), loss_scale)
+            w_lm = self._w(lm)
+            out.loss = ops.lm_head_ce(y, w_lm, self._g(lm), targets.reshape(-1), loss_scale,
+                                      wt=self._wt("lm_head", w_lm))
         if return_logits or (labels is None and targets is None):
             with torch.no_grad():
                 B, T = input_ids.shape

@@ -1,7 +1,8 @@
 """Hot-path ops.  Each op dispatches to a hand-written HIP/CDNA4 kernel for GPU tensors and to the
 PyTorch reference (``ops.reference``) for CPU tensors; see ``ops/_ext.py`` for the policy."""
 from ._ext import available as hip_available, set_backend, get_backend, ExtensionMissing
-from .linear import linear, wgrad_accumulate
+from .linear import linear, wgrad_accumulate, set_wgrad_overlap, wgrad_overlap_enabled, join_wgrad, \
+    set_dgrad_transposed, dgrad_transposed_enabled, transpose_into
 from .norm import rmsnorm, add_rmsnorm
 from .embedding import embedding
 from .swiglu import swiglu
@@ -11,5 +12,7 @@ from .optim import adamw_step, global_grad_norm, pseudograd, outer_nesterov
 from . import reference
 
 __all__ = ["hip_available", "set_backend", "get_backend", "ExtensionMissing", "linear", "wgrad_accumulate",
+           "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad",
+           "set_dgrad_transposed", "dgrad_transposed_enabled", "transpose_into",
            "rmsnorm", "add_rmsnorm", "embedding", "swiglu", "attention", "rope_cache", "lm_head_ce",
            "IGNORE_INDEX", "adamw_step", "global_grad_norm", "pseudograd", "outer_nesterov", "reference"]

@@ -25,7 +25,7 @@ from __future__ import annotations
 import torch
 
 from . import _ext
-from .linear import wgrad_accumulate
+from .linear import library_gemm_fence, wgrad_accumulate
 
 IGNORE_INDEX = -100
 
@@ -36,7 +36,7 @@ def _chunk_rows(V: int, elem: int, budget_bytes: int = 1 << 30) -> int:
 
 class LMHeadCEFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, w, gw, targets, loss_scale, chunk_rows):
+    def forward(ctx, y, w, gw, targets, loss_scale, chunk_rows, wt):
         n, d = y.shape
         V = w.shape[0]
         targets = targets.reshape(-1)
@@ -54,6 +54,7 @@ class LMHeadCEFn(torch.autograd.Function):
             e = min(n, s + chunk)
             yc, tc = y[s:e], targets[s:e]
             if hip:
+                library_gemm_fence(y.device)
                 logits = torch.mm(yc, w.t())
                 _ext.check(_ext.lib().nd_ce_fwd_bwd(_ext.ptr(logits), _ext.dtcode(logits), _ext.ptr(tc),
                                                     _ext.ptr(loss_sum), _ext.ptr(scale), e - s, V, IGNORE_INDEX,
@@ -70,8 +71,17 @@ class LMHeadCEFn(torch.autograd.Function):
                 p.scatter_add_(1, tgt[:, None], -torch.ones_like(p[:, :1]))
                 p *= ok[:, None].to(p.dtype) * scale
                 dl = p.to(y.dtype)
-            dy[s:e] = torch.mm(dl, w.to(dl.dtype))
+            # dy rows written in place (a row slice of a contiguous tensor); with wt = W^T the GEMM
+            # has the faster K-contiguous operand layout (ops/linear.py)
+            if wt is not None and dl.dtype == wt.dtype:
+                torch.mm(dl, wt.t(), out=dy[s:e])
+            elif dl.dtype == w.dtype:
+                torch.mm(dl, w, out=dy[s:e])
+            else:
+                dy[s:e] = torch.mm(dl, w.to(dl.dtype))
             if gw is not None:
+                # stays on the compute stream: the chunk loop is GEMM-bound (library GEMMs fence
+                # side-stream work anyway, ops/linear.py)
                 wgrad_accumulate(gw, dl, yc.to(dl.dtype))
         ctx.save_for_backward(dy)
         return (loss_sum / denom).reshape(())
@@ -79,9 +89,10 @@ class LMHeadCEFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (dy,) = ctx.saved_tensors
-        return dy * g.to(dy.dtype), None, None, None, None, None
+        return dy * g.to(dy.dtype), None, None, None, None, None, None
 
 
 def lm_head_ce(y: torch.Tensor, w: torch.Tensor, gw: torch.Tensor, targets: torch.Tensor,
-               loss_scale: float = 1.0, chunk_rows: int = 0) -> torch.Tensor:
-    return LMHeadCEFn.apply(y, w, gw, targets, float(loss_scale), int(chunk_rows))
+               loss_scale: float = 1.0, chunk_rows: int = 0, wt: torch.Tensor = None) -> torch.Tensor:
+    """``wt``: optional W^T copy [d, V] for the input-gradient GEMM (see ops/linear.py)."""
+    return LMHeadCEFn.apply(y, w, gw, targets, float(loss_scale), int(chunk_rows), wt)

@@ -40,6 +40,10 @@ class EmbeddingFn(torch.autograd.Function):
                                                        _ext.stream_ptr(dy.device)), "nd_embedding_bwd")
             else:
                 ctx.gw.index_add_(0, ids, dy.float())
+        # the embedding backward is the last op of the model's backward: join the side-stream
+        # weight-gradient GEMMs here so the grad buffer is complete on the compute stream
+        from .linear import join_wgrad
+        join_wgrad(dy.device if dy.is_cuda else None)
         return None, None, None, None
 
 

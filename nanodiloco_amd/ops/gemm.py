@@ -15,7 +15,10 @@ _WS = {}
 
 
 def _workspace(device, numel):
-    key = str(device)
+    """Split-K slab workspace, one per (device, stream): wgrads issued on the side stream
+    (ops/linear.py overlap) and on the compute stream (lm head) must not share slabs."""
+    stream = torch.cuda.current_stream(device)
+    key = (str(device), stream.cuda_stream)
     t = _WS.get(key)
     if t is None or t.numel() < numel:
         t = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)

@@ -7,6 +7,23 @@ tensor, no separate accumulate pass.  On the HIP path that GEMM is our own ``nd_
 (ops/gemm.py); otherwise hipBLASLt ``addmm(out_dtype=fp32)`` (this replaces autograd's per-parameter AccumulateGrad,
 K11 in SURVEY.md §2.3).  Fused weights (q|k|v, gate|up) are single views, so one GEMM covers
 all three / both projections.
+
+Weight-gradient overlap (``set_wgrad_overlap(True)``): the wgrad GEMM is off the backward's
+critical path (nothing downstream reads it until the optimizer), so it is issued on a side HIP
+stream forked from the compute stream at that point; the dgrad chain (dgrad GEMM -> SwiGLU /
+RMSNorm / attention backward, several of them HBM-bound) continues on the compute stream and the
+hardware co-schedules the two queues.  The compute stream joins the side stream at the end of the
+backward (``join_wgrad``: embedding backward, inner-DDP layer hooks, optimizer step) -- a GPU-side
+wait, never a host sync.  dY / X stay referenced until that join (then the compute stream, which
+allocated them, is ordered after the side stream, so the caching allocator may reuse them at once;
+``record_stream`` instead defers every such free behind an event and made the allocator fall
+back to fresh hipMalloc calls -- host stalls of hundreds of ms per step).
+
+GEMM fence: the compute stream also joins before every LIBRARY GEMM (``library_gemm_fence``).
+hipBLASLt's stream-K kernels keep one workgroup per CU and make workgroups wait on each other's
+partial tiles; when a side-stream wgrad holds CUs, part of that grid cannot become resident and
+the resident part spins -- measured 2-8x slower steps.  Fenced, a wgrad co-runs only with our own
+kernels (SwiGLU / RMSNorm backward, the attention backward), which never wait on each other.
 """
 from __future__ import annotations
 
@@ -15,6 +32,77 @@ import torch
 from . import _ext
 
 _DTYPE_OUT_OK = {"checked": False, "ok": False}
+_OVERLAP = {"enabled": False, "fence": True, "streams": {}, "pending": set(), "keep": []}
+_DGRAD_T = {"enabled": True}
+
+
+def transpose_into(dst: torch.Tensor, w: torch.Tensor) -> None:
+    """dst[in, out] = w[out, in]^T (bf16 HIP kernel on the GPU; strided copy otherwise)."""
+    if w.is_cuda and w.dtype == torch.bfloat16 and _ext.get_backend() != "torch":
+        _ext.check(_ext.lib().nd_transpose_bf16(_ext.ptr(w), _ext.ptr(dst), w.shape[0], w.shape[1], w.stride(0),
+                                                 dst.stride(0), _ext.stream_ptr(w.device)), "nd_transpose_bf16")
+    else:
+        dst.copy_(w.t())
+
+
+def set_dgrad_transposed(enabled: bool) -> None:
+    """Input-gradient GEMMs read a transposed weight copy (see ``LinearFn``)."""
+    _DGRAD_T["enabled"] = bool(enabled)
+
+
+def dgrad_transposed_enabled() -> bool:
+    return _DGRAD_T["enabled"]
+
+
+def set_wgrad_overlap(mode) -> None:
+    """Issue projection weight-gradient GEMMs on a side stream (GPU only).  0/False: off;
+    1/True: on, fenced before every library GEMM; 2: on, unfenced (A/B only, see module doc)."""
+    _OVERLAP["enabled"] = int(mode) != 0
+    _OVERLAP["fence"] = int(mode) != 2
+
+
+def wgrad_overlap_enabled() -> bool:
+    return _OVERLAP["enabled"]
+
+
+def _side_stream(device: torch.device) -> torch.cuda.Stream:
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    s = _OVERLAP["streams"].get(key)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _OVERLAP["streams"][key] = s
+    return s
+
+
+def join_wgrad(device=None) -> None:
+    """Make the current stream wait for every weight-gradient GEMM issued on the side stream
+    (no-op when nothing is outstanding)."""
+    if not _OVERLAP["pending"]:
+        return
+    keys = list(_OVERLAP["pending"]) if device is None else [
+        torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()]
+    for k in keys:
+        if k in _OVERLAP["pending"]:
+            torch.cuda.current_stream(k).wait_stream(_OVERLAP["streams"][k])
+            _OVERLAP["pending"].discard(k)
+    if not _OVERLAP["pending"]:
+        _OVERLAP["keep"].clear()  # operands of the joined wgrads: safe to free on the compute stream
+
+
+def library_gemm_fence(device=None) -> None:
+    """Call right before a hipBLASLt GEMM on the compute stream (see module doc: GEMM fence)."""
+    if _OVERLAP["pending"] and _OVERLAP["fence"]:
+        join_wgrad(device)
+
+
+def _wgrad_on_side_stream(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+    cur = torch.cuda.current_stream(gw.device)
+    side = _side_stream(gw.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        wgrad_accumulate(gw, dy, x)
+    _OVERLAP["keep"].append((dy, x))
+    _OVERLAP["pending"].add(side.device.index)
 
 
 def wgrad_accumulate(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor):
@@ -40,21 +128,35 @@ def wgrad_accumulate(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor):
 
 
 class LinearFn(torch.autograd.Function):
+    """``wt`` (optional) is W^T stored [in, out] contiguous: the input gradient is then dY . (W^T)^T,
+    the same K-contiguous "NT" operand layout as the forward GEMM, which hipBLASLt runs 14-16 %
+    faster than dY . W (row-major x row-major) on every Llama-150M shape
+    (scripts/dgrad_layout_bench.py); the model keeps the copies in step with the optimizer."""
+
     @staticmethod
-    def forward(ctx, x, w, gw):
-        ctx.save_for_backward(x, w)
+    def forward(ctx, x, w, gw, wt=None):
+        ctx.save_for_backward(x, w if wt is None else wt)
         ctx.gw = gw
+        ctx.transposed = wt is not None
+        library_gemm_fence(x.device if x.is_cuda else None)
         return torch.mm(x, w.t())
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dy = dy.contiguous()
-        dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
+        if ctx.needs_input_grad[0]:
+            library_gemm_fence(dy.device if dy.is_cuda else None)
+            dx = torch.mm(dy, w.t()) if ctx.transposed else torch.mm(dy, w)
+        else:
+            dx = None
         if ctx.gw is not None:
-            wgrad_accumulate(ctx.gw, dy, x)
-        return dx, None, None
+            if _OVERLAP["enabled"] and ctx.gw.is_cuda:
+                _wgrad_on_side_stream(ctx.gw, dy, x)
+            else:
+                wgrad_accumulate(ctx.gw, dy, x)
+        return dx, None, None, None
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, gw: torch.Tensor) -> torch.Tensor:
-    return LinearFn.apply(x, w, gw)
+def linear(x: torch.Tensor, w: torch.Tensor, gw: torch.Tensor, wt: torch.Tensor = None) -> torch.Tensor:
+    return LinearFn.apply(x, w, gw, wt)

@@ -41,6 +41,7 @@ class FlatAdamW:
         lr = self.lr if lr is None else lr
         self.param_groups[0]["lr"] = lr
         self.step_count += 1
+        ops.join_wgrad()
         ops.adamw_step(self.store.master, self.store.grad, self.exp_avg, self.exp_avg_sq, self.store.shadow,
                        self.step_count, lr, self.betas, self.eps, self.weight_decay, self.max_grad_norm,
                        norm_out=self.last_grad_norm, skip_nonfinite=self.skip_nonfinite,
@@ -48,6 +49,7 @@ class FlatAdamW:
         self.store.version += 1
 
     def zero_grad(self, set_to_none: bool = False):
+        ops.join_wgrad()
         self.store.zero_grad()
 
     def state_dict(self):

@@ -67,6 +67,8 @@ class TrainArgs:
     fp8: bool = False              # fp8 e4m3/e5m2 decoder projections (GPU, bf16 compute)
     tuned_gemm: bool = True        # load the pre-tuned hipBLASLt algorithm table (ops/tuned_gemm.py)
     hip_graph: bool = False        # capture the micro-batch fwd+bwd in a HIP graph (utils/graphs.py)
+    wgrad_overlap: bool = False    # weight-gradient GEMMs on a side HIP stream (ops/linear.py; GPU only;
+                                   # off: co-running with hipBLASLt stream-K GEMMs stalls, docs/DESIGN.md)
     checkpoint_dir: Optional[str] = None
     checkpoint_every: int = 0      # in outer steps (0 = only at the end when checkpoint_dir is set)
     stop_at_step: int = 0          # stop early (simulated preemption) after this inner step; 0 = run to total
@@ -111,6 +113,7 @@ class Trainer:
         if a.total_steps % a.inner_steps:
             raise ValueError("total_steps must be a multiple of inner_steps")  # REF main.py:69
         ops.set_backend(a.ops)
+        ops.set_wgrad_overlap(a.wgrad_overlap)
         self.env = env or init_distributed(a.backend, a.inner_dp, device=None if a.device == "auto" else a.device,
                                            timeout_s=a.collective_timeout_s)
         e = self.env

@@ -52,11 +52,13 @@ class GraphedMicroStep:
             return self._run(ids, labels, loss_scale)
         if self.graph is None:
             self.ids, self.labels, self.loss_scale = ids.clone(), labels.clone(), loss_scale
+            self.model.refresh_transposed()  # nothing stale gets captured as a copy
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):  # records only; the replay below does the work
                 self.loss = self._run(self.ids, self.labels, loss_scale)
         if loss_scale != self.loss_scale:
             raise ValueError("loss_scale changed after capture")
+        self.model.refresh_transposed()  # W^T copies the captured dgrad GEMMs read
         self.ids.copy_(ids, non_blocking=True)
         self.labels.copy_(labels, non_blocking=True)
         self.graph.replay()

@@ -8,7 +8,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 set -o pipefail
 step() { local name=$1; shift; local t=$1; shift; echo "== $name"; timeout -k 10 $t "$@" > gpurun_out/$name.log 2>&1; local rc=$?; tail -${TAILN:-4} gpurun_out/$name.log; echo "== $name rc=$rc"; return $rc; }
 if [ -z "$SKIP_TESTS" ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x; rc=$?
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider -x --timeout 300 --timeout-method thread; rc=$?
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi
 step bench_hip 600 python bench.py --steps ${STEPS:-5} --warmup 2 ${BENCH_ARGS} || exit $?

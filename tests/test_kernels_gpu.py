@@ -312,3 +312,25 @@ def test_gemm_nt(M, N, K):
     _ext.check(_ext.lib().nd_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, K, K, N, 0,
                                      _ext.stream_ptr()), "nd_gemm_nt")
     assert rel(c, a.float() @ b.float().t()) < 5e-3
+
+
+# ----------------------------------------------------------------------------------- transpose
+@pytest.mark.parametrize("rows,cols", [(3072, 1024), (1024, 2688), (100, 72), (32000, 1024)])
+def test_transpose_bf16(rows, cols):
+    """W^T copies for the input-gradient GEMMs: exact (a permutation), edge tiles included."""
+    w = torch.randn(rows, cols, device=DEV).bfloat16()
+    out = torch.empty(cols, rows, device=DEV, dtype=torch.bfloat16)
+    ops.transpose_into(out, w)
+    assert torch.equal(out, w.t())
+
+
+@pytest.mark.parametrize("rows", [1024, 700])
+def test_colsum_add(rows):
+    """RMSNorm dW partial-row reduction into the flat grad (fixed order, += into existing)."""
+    from nanodiloco_amd.ops import _ext
+    cols = 1024
+    part = torch.randn(rows, cols, device=DEV)
+    out = torch.randn(cols, device=DEV)
+    ref_ = out.double() + part.double().sum(0)
+    _ext.check(_ext.lib().nd_colsum_add(part.data_ptr(), out.data_ptr(), rows, cols, _ext.stream_ptr()), "colsum")
+    assert rel(out, ref_) < 1e-6

@@ -84,3 +84,109 @@ def test_hip_graph_matches_eager():
         assert abs(a - b) < 1e-4 * abs(a), (losses1, losses2)
     rel = ((m1.store.grad - m2.store.grad).norm() / m1.store.grad.norm()).item()
     assert rel < 1e-4, rel
+
+
+def _trajectory(cfg, batches, graphed, seed=5):
+    """Losses, the grad of the last accumulated micro-batch pair and the final weights of a few
+    micro-batches with an optimizer step every second one."""
+    from nanodiloco_amd.utils.graphs import GraphedMicroStep
+    m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16).init_weights(seed)
+    opt = FlatAdamW(m.store, lr=1e-3)
+    g = GraphedMicroStep(m) if graphed else None
+    losses, grad = [], None
+    for i, ids in enumerate(batches):
+        if g is not None:
+            losses.append(g(ids, ids, 0.5).clone())
+        else:
+            out = m(ids, labels=ids, loss_scale=0.5)
+            out.loss.backward()
+            losses.append(out.loss.detach())
+        if i % 2 == 1:
+            grad = m.store.grad.clone()
+            opt.step()
+            opt.zero_grad()
+    torch.cuda.synchronize()
+    return torch.stack(losses).cpu(), grad, m.store.master.clone()
+
+
+def _rel(a, b):
+    return ((a - b).float().norm() / b.float().norm()).item()
+
+
+def _schedule_check(cfg, batches, graphed, switch):
+    """Run the reference schedule twice (its own run-to-run spread: hipBLASLt stream-K GEMMs and the
+    embedding's float atomics are not bitwise reproducible) and the switched schedule once; the
+    switched run must sit within a small multiple of that spread."""
+    switch(False)
+    l0, g0, p0 = _trajectory(cfg, batches, graphed)
+    l0b, g0b, p0b = _trajectory(cfg, batches, graphed)
+    switch(True)
+    try:
+        l1, g1, p1 = _trajectory(cfg, batches, graphed)
+    finally:
+        switch(False)
+    tol_g = max(4 * _rel(g0b, g0), 1e-4)
+    tol_p = max(4 * _rel(p0b, p0), 1e-6)
+    tol_l = max(4 * (l0b - l0).abs().max().item(), 1e-5)
+    assert (l1 - l0).abs().max().item() <= tol_l, (l0, l0b, l1)
+    assert _rel(g1, g0) <= tol_g, (_rel(g1, g0), _rel(g0b, g0))
+    assert _rel(p1, p0) <= tol_p, (_rel(p1, p0), _rel(p0b, p0))
+
+
+_CFG_SMALL = dict(hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2,
+                  num_hidden_layers=3, vocab_size=1000)
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_wgrad_overlap_matches_serial(graphed):
+    """Weight-gradient GEMMs on the side stream (fork/join; also inside a captured HIP graph) give
+    the serial schedule's gradients and optimizer trajectory.  A missing join (a read of a
+    half-written gradient) lands orders of magnitude outside the run-to-run spread."""
+    ops.set_backend("hip")
+    cfg = LlamaConfig.from_dict(_CFG_SMALL)
+    batches = [torch.randint(0, 1000, (4, 256), device="cuda") for _ in range(6)]
+    _schedule_check(cfg, batches, graphed, ops.set_wgrad_overlap)
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_dgrad_transposed_weights(graphed):
+    """Input gradients through the W^T copies: every cached copy equals the CURRENT weights' transpose
+    after optimizer steps (refreshed lazily in eager mode, and before every HIP-graph replay), and
+    the trajectory matches the plain-layout dgrad within bf16 rounding (the NT and NN GEMM kernels
+    round differently, so not within the run-to-run spread)."""
+    from nanodiloco_amd.utils.graphs import GraphedMicroStep
+    ops.set_backend("hip")
+    cfg = LlamaConfig.from_dict(_CFG_SMALL)
+    batches = [torch.randint(0, 1000, (4, 256), device="cuda") for _ in range(7)]
+    prev = ops.dgrad_transposed_enabled()
+    try:
+        ops.set_dgrad_transposed(False)
+        l0, g0, p0 = _trajectory(cfg, batches, graphed)
+        ops.set_dgrad_transposed(True)
+        l1, g1, p1 = _trajectory(cfg, batches, graphed)
+        # freshness of the copies after 3 optimizer steps + one more micro-batch
+        m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16).init_weights(5)
+        opt = FlatAdamW(m.store, lr=1e-3)
+        g = GraphedMicroStep(m) if graphed else None
+        for ids in batches:
+            if g is not None:
+                g(ids, ids, 0.5)
+            else:
+                m(ids, labels=ids, loss_scale=0.5).loss.backward()
+            opt.step()
+            opt.zero_grad()
+        ids = batches[0]
+        if g is not None:
+            g(ids, ids, 0.5)
+        else:
+            m(ids, labels=ids, loss_scale=0.5).loss.backward()
+        torch.cuda.synchronize()
+        assert len(m._wt_cache) == 4 * cfg.num_hidden_layers + 1
+        for key, (wt, ver, w) in m._wt_cache.items():
+            assert ver == m.store.version, key
+            assert torch.equal(wt, w.t()), key
+    finally:
+        ops.set_dgrad_transposed(prev)
+    assert ((l1 - l0).abs() / l0.abs()).max().item() < 1e-3, (l0, l1)
+    assert _rel(g1, g0) < 2e-2
+    assert _rel(p1, p0) < 5e-4
