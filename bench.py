@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=128.0)
     ap.add_argument("--overlap-outer", action="store_true")
     ap.add_argument("--no-tuned-gemm", action="store_true", help="library-default GEMM algorithms (A/B)")
+    ap.add_argument("--tuned-gemm-file", default=None, help="alternative TunableOp table (A/B of tunings)")
     ap.add_argument("--hip-graph", action="store_true",
                     help="capture the micro-batch forward+backward in a HIP graph (launch-bound small models)")
     ap.add_argument("--wgrad-overlap", type=int, default=0, choices=[0, 1, 2],
@@ -83,7 +84,10 @@ def main():
     if env.world_size != a.gpus and env.rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
     if env.device.type == "cuda" and not a.no_tuned_gemm:
-        enable_tuned_gemms(env.device)
+        if a.tuned_gemm_file:
+            enable_tuned_gemms(env.device, a.tuned_gemm_file)
+        else:
+            enable_tuned_gemms(env.device)
     cfg = resolve_llama_config(a.model)
     dtype = torch.bfloat16 if env.device.type == "cuda" else torch.float32
     model = LlamaForCausalLM(cfg, env.device, dtype, fp8=a.fp8, fp8_wgrad=a.fp8_wgrad).init_weights(1337)
