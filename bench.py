@@ -38,6 +38,7 @@ from nanodiloco_amd.parallel.dist import barrier, init_distributed  # noqa: E402
 from nanodiloco_amd.parallel.inner_ddp import InnerGradSync  # noqa: E402
 
 BASELINE_TOKENS_PER_S = None  # the reference publishes no number
+METRIC = "tokens/sec (whole node) Llama-150M, 8 DiLoCo workers H=100; bytes/outer-step"  # BASELINE.json
 MODEL_NAMES = {"llama_150m": "Llama-150M", "llama_1b": "Llama-1B", "llama_default": "Llama-10M (reference default)",
                "llama_tiny": "tiny-Llama-2L", "llama_large": "Llama-29M"}
 
@@ -170,9 +171,11 @@ def main():
             sync()
         print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=30), file=sys.stderr)
     if env.rank == 0:
+        model_name = MODEL_NAMES.get(os.path.splitext(os.path.basename(a.model))[0], a.model)
         mfu_flops = cfg.flops_per_token(a.seq_len) * tps / max(1, env.world_size)
         out = {
-            "metric": "tokens/sec (whole node) Llama-150M, 8 DiLoCo workers H=100; bytes/outer-step",
+            "metric": METRIC if model_name == "Llama-150M" else
+            f"tokens/sec (whole node) {model_name}, DiLoCo workers H={a.inner_steps}",
             "value": round(tps, 1),
             "unit": "tokens/s",
             "n_gpus": env.world_size,
@@ -185,7 +188,7 @@ def main():
             "dtype": ("fp8" if a.fp8 else "bf16") if dtype == torch.bfloat16 else "fp32",
             "data": "synthetic",
             "config": {
-                "model": MODEL_NAMES.get(os.path.splitext(os.path.basename(a.model))[0], a.model),
+                "model": model_name,
                 "global_batch": a.batch_size * env.world_size,
                 "seq_len": a.seq_len,
                 "parallelism": f"diloco{env.num_workers}" + (f"x_ddp{env.inner_dp}" if env.inner_dp > 1 else ""),

@@ -125,9 +125,11 @@ def _schedule_check(cfg, batches, graphed, switch):
         l1, g1, p1 = _trajectory(cfg, batches, graphed)
     finally:
         switch(False)
-    tol_g = max(4 * _rel(g0b, g0), 1e-4)
-    tol_p = max(4 * _rel(p0b, p0), 1e-6)
-    tol_l = max(4 * (l0b - l0).abs().max().item(), 1e-5)
+    # floors at bf16-rounding level: a read of a half-written gradient moves the affected weights by
+    # ~lr in a wrong direction (>= 1e-2 relative on them), far above these
+    tol_g = max(4 * _rel(g0b, g0), 1e-3)
+    tol_p = max(4 * _rel(p0b, p0), 1e-4)
+    tol_l = max(4 * (l0b - l0).abs().max().item(), 2e-4)
     assert (l1 - l0).abs().max().item() <= tol_l, (l0, l0b, l1)
     assert _rel(g1, g0) <= tol_g, (_rel(g1, g0), _rel(g0b, g0))
     assert _rel(p1, p0) <= tol_p, (_rel(p1, p0), _rel(p0b, p0))
