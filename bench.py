@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--wgrad-overlap", type=int, default=0, choices=[0, 1, 2],
                     help="issue weight-gradient GEMMs on a side HIP stream (overlaps the dgrad chain); off by "
                          "default: beside hipBLASLt's stream-K GEMMs it stalls (docs/DESIGN.md)")
+    ap.add_argument("--wgrad-variant", default=None,
+                    help="ND_WGRAD_VARIANT for the weight-gradient kernel (A/B of kernel schedules)")
     ap.add_argument("--dgrad-t", type=int, default=1, choices=[0, 1],
                     help="input-gradient GEMMs on transposed weight copies (K-contiguous NT layout)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
@@ -81,6 +83,8 @@ def main():
     ops.set_backend(a.ops)
     ops.set_wgrad_overlap(a.wgrad_overlap)
     ops.set_dgrad_transposed(bool(a.dgrad_t))
+    if a.wgrad_variant:
+        os.environ["ND_WGRAD_VARIANT"] = a.wgrad_variant
     env = init_distributed(a.backend, a.inner_dp)
     if env.world_size != a.gpus and env.rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
