@@ -112,14 +112,14 @@ def build(force: bool = False, jobs: int = 0, save_temps: bool = False, verbose:
     return {"kernels": kern, "runtime": rt, "compiled": [os.path.basename(s) for s, _ in todo]}
 
 
-def build_revision(rev: str, jobs: int = 0) -> str:
+def build_revision(rev: str, jobs: int = 0, extra_flags=None, file_flags: bool = True, tag: str = "") -> str:
     """Build libnd_kernels.so from the csrc/ of git revision `rev` into _lib/alt/ (for in-process
     A/B against the working tree: device-to-device and run-to-run variance on MI355X is several
     percent, so code versions are compared interleaved inside one process; see scripts/ab_kernels.py)."""
     import tempfile
     root = os.path.dirname(PKG)
     sha = _run(["git", "-C", root, "rev-parse", "--short", rev]).stdout.strip()
-    out = os.path.join(LIB_DIR, "alt", f"libnd_kernels_{sha}.so")
+    out = os.path.join(LIB_DIR, "alt", f"libnd_kernels_{sha}{('_' + tag) if tag else ''}.so")
     if os.path.exists(out):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
@@ -135,10 +135,12 @@ def build_revision(rev: str, jobs: int = 0) -> str:
                 if n.endswith(".hip"):
                     srcs.append(dst)
         flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-I", td]
+        flags += list(extra_flags or [])
 
         def comp(src):
             o = src + ".o"
-            _run([hipcc] + flags + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", o])
+            ff = FILE_FLAGS.get(os.path.basename(src), []) if file_flags else []
+            _run([hipcc] + flags + ff + ["-c", src, "-o", o])
             return o
 
         with cf.ThreadPoolExecutor(max_workers=jobs or min(8, os.cpu_count() or 4)) as ex:
@@ -155,9 +157,12 @@ def main(argv=None):
     ap.add_argument("--jobs", type=int, default=0)
     ap.add_argument("--save-temps", action="store_true")
     ap.add_argument("--rev", default=None, help="build the kernels of this git revision into _lib/alt/ (A/B)")
+    ap.add_argument("--extra-flags", default="", help="with --rev: extra hipcc flags (compiler-option A/B)")
+    ap.add_argument("--no-file-flags", action="store_true", help="with --rev: drop the per-file flags")
+    ap.add_argument("--tag", default="", help="with --rev: suffix of the side library's file name")
     a = ap.parse_args(argv)
     if a.rev:
-        print(build_revision(a.rev, a.jobs))
+        print(build_revision(a.rev, a.jobs, a.extra_flags.split(), not a.no_file_flags, a.tag))
         return
     out = build(force=a.force, jobs=a.jobs, save_temps=a.save_temps, verbose=True)
     print(out)

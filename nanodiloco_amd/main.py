@@ -17,6 +17,9 @@ from typing import List, Optional
 from .trainer import TrainArgs, Trainer
 
 
+TRISTATE = {"hip_graph"}  # on | off | auto; the bare flag means "on"
+
+
 def _bool(s: str) -> bool:
     return s.lower() in ("1", "true", "yes", "on")
 
@@ -32,6 +35,8 @@ def build_parser() -> argparse.ArgumentParser:
             p.add_argument(flag, type=int, default=default)
         elif f.type in (float, "float"):
             p.add_argument(flag, type=float, default=default)
+        elif f.name in TRISTATE:
+            p.add_argument(flag, type=str, nargs="?", const="on", default=default)  # bare flag = on
         else:
             p.add_argument(flag, type=str, default=default)
     return p

@@ -66,7 +66,9 @@ class TrainArgs:
     activation_checkpointing: bool = False
     fp8: bool = False              # fp8 e4m3/e5m2 decoder projections (GPU, bf16 compute)
     tuned_gemm: bool = True        # load the pre-tuned hipBLASLt algorithm table (ops/tuned_gemm.py)
-    hip_graph: bool = False        # capture the micro-batch fwd+bwd in a HIP graph (utils/graphs.py)
+    hip_graph: str = "auto"        # capture the micro-batch fwd+bwd in a HIP graph (utils/graphs.py):
+                                   # on | off | auto (= on for launch-bound models: GPU, < 100M params,
+                                   # --inner-dp 1, no fp8, e.g. the reference's 10M default: 2.5x)
     wgrad_overlap: bool = False    # weight-gradient GEMMs on a side HIP stream (ops/linear.py; GPU only;
                                    # off: co-running with hipBLASLt stream-K GEMMs stalls, docs/DESIGN.md)
     checkpoint_dir: Optional[str] = None
@@ -154,7 +156,13 @@ class Trainer:
                 except Exception:
                     pass
         self.graphed = None
-        if a.hip_graph:
+        hg = str(a.hip_graph).lower()
+        if hg == "auto":
+            use_graph = (e.device.type == "cuda" and e.inner_dp == 1 and self.model.fp8 is None
+                         and self.llama_config.num_params() < 100_000_000)
+        else:
+            use_graph = hg in ("1", "true", "on", "yes")
+        if use_graph:
             if e.device.type != "cuda" or e.inner_dp > 1 or self.model.fp8 is not None:
                 raise ValueError("--hip-graph needs a GPU, --inner-dp 1 and no --fp8")
             from .utils.graphs import GraphedMicroStep
