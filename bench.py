@@ -74,6 +74,8 @@ def parse():
                     help="input-gradient GEMMs on transposed weight copies (K-contiguous NT layout)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
     ap.add_argument("--fp8-wgrad", action="store_true", help="with --fp8: weight-gradient GEMM in fp8 too")
+    ap.add_argument("--fp8-fused-quant", type=int, default=1, choices=[0, 1],
+                    help="with --fp8: operand quantisation fused into the producing kernels (0: separate casts)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
     return ap.parse_args()
 
@@ -83,6 +85,9 @@ def main():
     ops.set_backend(a.ops)
     ops.set_wgrad_overlap(a.wgrad_overlap)
     ops.set_dgrad_transposed(bool(a.dgrad_t))
+    if a.fp8:
+        from nanodiloco_amd.ops import fp8 as _fp8
+        _fp8.set_fused_quant(bool(a.fp8_fused_quant))
     if a.wgrad_variant:
         os.environ["ND_WGRAD_VARIANT"] = a.wgrad_variant
     env = init_distributed(a.backend, a.inner_dp)

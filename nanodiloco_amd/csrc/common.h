@@ -91,6 +91,73 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// ---- OCP fp8 (gfx950 v_cvt_pk_fp8_f32 / v_cvt_pk_bf8_f32: e4m3fn / e5m2, RNE), saturating
+template <int FMT>  // 0: e4m3 (max 448), 1: e5m2 (max 57344)
+__device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d) {
+  constexpr float FMAX = FMT == 0 ? 448.f : 57344.f;
+  a = fminf(fmaxf(a, -FMAX), FMAX);
+  b = fminf(fmaxf(b, -FMAX), FMAX);
+  c = fminf(fmaxf(c, -FMAX), FMAX);
+  d = fminf(fmaxf(d, -FMAX), FMAX);
+  int r;
+  if (FMT == 0) {
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+  } else {
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, r, true);
+  }
+  return (uint32_t)r;
+}
+
+// Fused fp8 side output of a bf16-producing kernel (the fp8 inner step's operand quantisation
+// folded into the producer): q[i] = fp8(bf16(v[i]) * scale), amax of |bf16(v[i])| -- bitwise the
+// separate nd_fp8_cast pass over the bf16 tensor.  q == nullptr: no side output.
+struct Fp8Out {
+  uint8_t* q;
+  const float* scale;  // device scalar (delayed scaling: known before the producer runs)
+  float* amax;         // `parts` partial maxima (float bits as ordered ints), block b -> b % parts
+  int parts;
+  int fmt;             // 0 e4m3, 1 e5m2
+};
+
+// v: 8 fp32 values already rounded to bf16; writes 8 fp8 bytes at q + off, folds |v| into amax
+__device__ __forceinline__ void fp8_put8(const Fp8Out& f, int64_t off, const float* v, float& amax) {
+  const float sc = f.scale[0];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+  uint2 o;
+  if (f.fmt == 0) {
+    o.x = cvt4<0>(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc);
+    o.y = cvt4<0>(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc);
+  } else {
+    o.x = cvt4<1>(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc);
+    o.y = cvt4<1>(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc);
+  }
+  *reinterpret_cast<uint2*>(f.q + off) = o;
+}
+
+__device__ __forceinline__ void round_bf16x8(float* v) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j]));
+}
+
+// Block-wide amax -> one atomicMax into a partial slot.  Every thread of the block must call it
+// (it contains barriers); NT = block size.  Non-negative floats order like their int bits.
+template <int NT>
+__device__ __forceinline__ void block_amax_commit(float amax, float* amax_out, int parts) {
+  __shared__ float red_amax[NT / 64];
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0) red_amax[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = red_amax[0];
+#pragma unroll
+    for (int i = 1; i < NT / 64; ++i) m = fmaxf(m, red_amax[i]);
+    atomicMax(reinterpret_cast<int*>(amax_out + blockIdx.x % parts), __float_as_int(m));
+  }
+}
+
 }  // namespace nd
 
 #define ND_LAUNCH_CHECK() return (int)hipGetLastError()

@@ -11,23 +11,7 @@
 
 using namespace nd;
 
-template <int FMT>  // 0: e4m3 (max 448), 1: e5m2 (max 57344)
-__device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d) {
-  constexpr float FMAX = FMT == 0 ? 448.f : 57344.f;
-  a = fminf(fmaxf(a, -FMAX), FMAX);
-  b = fminf(fmaxf(b, -FMAX), FMAX);
-  c = fminf(fmaxf(c, -FMAX), FMAX);
-  d = fminf(fmaxf(d, -FMAX), FMAX);
-  int r;
-  if (FMT == 0) {
-    r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-    r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
-  } else {
-    r = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
-    r = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, r, true);
-  }
-  return (uint32_t)r;
-}
+// cvt4 (saturating OCP fp8 conversion of 4 floats): common.h
 
 template <int XDT, int FMT>
 __global__ void __launch_bounds__(256) fp8_cast_kernel(const void* __restrict__ x, int64_t n,
@@ -41,15 +25,17 @@ __global__ void __launch_bounds__(256) fp8_cast_kernel(const void* __restrict__ 
     Vec8<XDT>::load(x, i * 8, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
-    uint2 o;
-    o.x = cvt4<FMT>(v[0] * scale, v[1] * scale, v[2] * scale, v[3] * scale);
-    o.y = cvt4<FMT>(v[4] * scale, v[5] * scale, v[6] * scale, v[7] * scale);
-    *reinterpret_cast<uint2*>(out + i * 8) = o;
+    if (out) {  // out == nullptr: amax-only pass (weights use current scaling: amax first, then cast)
+      uint2 o;
+      o.x = cvt4<FMT>(v[0] * scale, v[1] * scale, v[2] * scale, v[3] * scale);
+      o.y = cvt4<FMT>(v[4] * scale, v[5] * scale, v[6] * scale, v[7] * scale);
+      *reinterpret_cast<uint2*>(out + i * 8) = o;
+    }
   }
   for (int64_t i = n8 * 8 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float f = XDT == BF16 ? bf2f(reinterpret_cast<const bf16_t*>(x)[i]) : reinterpret_cast<const float*>(x)[i];
     amax = fmaxf(amax, fabsf(f));
-    out[i] = (uint8_t)(cvt4<FMT>(f * scale, 0.f, 0.f, 0.f) & 0xff);
+    if (out) out[i] = (uint8_t)(cvt4<FMT>(f * scale, 0.f, 0.f, 0.f) & 0xff);
   }
   if (amax_out) {
     __shared__ float red[4];

@@ -12,11 +12,13 @@
 
 using namespace nd;
 
-template <int NCH, int XDT, int ADT, int YDT>
+// Q (YDT == BF16 only): fused fp8 side output of y for the fp8 inner step (common.h Fp8Out).
+template <int NCH, int XDT, int ADT, int YDT, bool Q = false>
 __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const void* __restrict__ x, const void* __restrict__ a,
                                                           const float* __restrict__ w, void* __restrict__ y,
                                                           float* __restrict__ h_out, float* __restrict__ rstd_out,
-                                                          int64_t rows, int cols, float eps) {
+                                                          int64_t rows, int cols, float eps, Fp8Out q8) {
+  float qmax = 0.f;
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * 4;
@@ -52,17 +54,24 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const void* __restrict
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = wv[j] * (v[c][j] * rs);
         Vec8<YDT>::store(y, base + col, o);
+        if (Q) {
+          round_bf16x8(o);
+          fp8_put8(q8, base + col, o, qmax);
+        }
       }
     }
   }
+  if (Q) block_amax_commit<256>(qmax, q8.amax, q8.parts);
 }
 
-template <int NCH, int DYDT, int DADT>
+// Q (DADT == BF16 only): fused fp8 side output of the branch gradient da (common.h Fp8Out).
+template <int NCH, int DYDT, int DADT, bool Q = false>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const void* __restrict__ dy, const float* __restrict__ h,
                                                           const float* __restrict__ w, const float* __restrict__ rstd,
                                                           const float* __restrict__ dres, float* __restrict__ dx,
                                                           void* __restrict__ da, float* __restrict__ part,
-                                                          int64_t rows, int cols) {
+                                                          int64_t rows, int cols, Fp8Out q8) {
+  float qmax = 0.f;
   extern __shared__ __attribute__((aligned(16))) float sdw[];
   const int lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < cols; i += 256) sdw[i] = 0.f;
@@ -116,9 +125,14 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const void* __restrict
         for (int j = 0; j < 8; ++j) o[j] += rs * (g[c][j] - xh[c][j] * dot);
         Vec8<F32>::store(dx, base + col, o);
         if (DADT >= 0) Vec8<(DADT >= 0 ? DADT : 0)>::store(da, base + col, o);
+        if (Q) {
+          round_bf16x8(o);
+          fp8_put8(q8, base + col, o, qmax);
+        }
       }
     }
   }
+  if (Q) block_amax_commit<256>(qmax, q8.amax, q8.parts);
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = (c * 64 + lane) * 8;
@@ -133,11 +147,22 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const void* __restrict
 // ------------------------------------------------------------------------------------ launchers
 template <int NCH>
 static int fwd_dispatch(const void* x, int xdt, const void* a, int adt, const float* w, void* y, int ydt, float* h,
-                        float* rstd, int64_t rows, int cols, float eps, hipStream_t s) {
+                        float* rstd, int64_t rows, int cols, float eps, hipStream_t s, const Fp8Out* q8 = nullptr) {
   int64_t blocks = (rows + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   dim3 g((unsigned)blocks), b(256);
-#define ND_RF(X, A, Y) hipLaunchKernelGGL((rmsnorm_fwd_kernel<NCH, X, A, Y>), g, b, 0, s, x, a, w, y, h, rstd, rows, cols, eps)
+  const Fp8Out none{nullptr, nullptr, nullptr, 1, 0};
+  if (q8) {  // fused fp8 side output: bf16 y only
+    if (ydt != BF16 || xdt != F32 || (a != nullptr && adt != BF16)) return (int)hipErrorInvalidValue;
+    if (a == nullptr)
+      hipLaunchKernelGGL((rmsnorm_fwd_kernel<NCH, F32, -1, BF16, true>), g, b, 0, s, x, a, w, y, h, rstd, rows, cols,
+                         eps, *q8);
+    else
+      hipLaunchKernelGGL((rmsnorm_fwd_kernel<NCH, F32, BF16, BF16, true>), g, b, 0, s, x, a, w, y, h, rstd, rows, cols,
+                         eps, *q8);
+    ND_LAUNCH_CHECK();
+  }
+#define ND_RF(X, A, Y) hipLaunchKernelGGL((rmsnorm_fwd_kernel<NCH, X, A, Y>), g, b, 0, s, x, a, w, y, h, rstd, rows, cols, eps, none)
   if (a == nullptr) {
     if (xdt == F32 && ydt == BF16) ND_RF(F32, -1, BF16);
     else if (xdt == F32 && ydt == F32) ND_RF(F32, -1, F32);
@@ -167,12 +192,20 @@ ND_API int nd_rmsnorm_fwd(const void* x, int xdt, const void* a, int adt, const 
 
 template <int NCH>
 static int bwd_dispatch(const void* dy, int dydt, const float* h, const float* w, const float* rstd, const float* dres,
-                        float* dx, int dadt, void* da, int64_t rows, int cols, float* part, hipStream_t s) {
+                        float* dx, int dadt, void* da, int64_t rows, int cols, float* part, hipStream_t s,
+                        const Fp8Out* q8 = nullptr) {
   int64_t blocks = (rows + 63) / 64;
   if (blocks > 1024) blocks = 1024;
   dim3 g((unsigned)blocks), b(256);
   size_t lds = (size_t)cols * sizeof(float);
-#define ND_RB(D, A) hipLaunchKernelGGL((rmsnorm_bwd_kernel<NCH, D, A>), g, b, lds, s, dy, h, w, rstd, dres, dx, da, part, rows, cols)
+  const Fp8Out none{nullptr, nullptr, nullptr, 1, 0};
+  if (q8) {  // fused fp8 side output: bf16 dy and da only
+    if (dydt != BF16 || dadt != BF16 || da == nullptr) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((rmsnorm_bwd_kernel<NCH, BF16, BF16, true>), g, b, lds, s, dy, h, w, rstd, dres, dx, da, part,
+                       rows, cols, *q8);
+    ND_LAUNCH_CHECK();
+  }
+#define ND_RB(D, A) hipLaunchKernelGGL((rmsnorm_bwd_kernel<NCH, D, A>), g, b, lds, s, dy, h, w, rstd, dres, dx, da, part, rows, cols, none)
   if (da == nullptr) {
     if (dydt == BF16) ND_RB(BF16, -1); else ND_RB(F32, -1);
   } else {
@@ -196,6 +229,33 @@ ND_API int nd_rmsnorm_bwd(const void* dy, int dydt, const float* h, const float*
     case 2: return bwd_dispatch<2>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
     case 3: case 4: return bwd_dispatch<4>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
     default: return bwd_dispatch<8>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
+  }
+}
+
+// fp8 inner step: the same launchers with the fused fp8 side output (q: fp8 bytes shaped like y / da).
+ND_API int nd_rmsnorm_fwd_q(const void* x, int xdt, const void* a, int adt, const float* w, void* y, int ydt, float* h,
+                            float* rstd, int64_t rows, int cols, float eps, void* q, const float* scale, float* amax,
+                            int parts, int fmt, hipStream_t s) {
+  if (cols % 8 || cols > 8 * 512 || !q || !scale || !amax || parts < 1) return (int)hipErrorInvalidValue;
+  const Fp8Out q8{(uint8_t*)q, scale, amax, parts, fmt};
+  switch ((cols + 511) / 512) {
+    case 1: return fwd_dispatch<1>(x, xdt, a, adt, w, y, ydt, h, rstd, rows, cols, eps, s, &q8);
+    case 2: return fwd_dispatch<2>(x, xdt, a, adt, w, y, ydt, h, rstd, rows, cols, eps, s, &q8);
+    case 3: case 4: return fwd_dispatch<4>(x, xdt, a, adt, w, y, ydt, h, rstd, rows, cols, eps, s, &q8);
+    default: return fwd_dispatch<8>(x, xdt, a, adt, w, y, ydt, h, rstd, rows, cols, eps, s, &q8);
+  }
+}
+
+ND_API int nd_rmsnorm_bwd_q(const void* dy, int dydt, const float* h, const float* w, const float* rstd,
+                            const float* dres, float* dx, int dadt, void* da, int64_t rows, int cols, float* part,
+                            void* q, const float* scale, float* amax, int parts, int fmt, hipStream_t s) {
+  if (cols % 8 || cols > 8 * 512 || !q || !scale || !amax || parts < 1) return (int)hipErrorInvalidValue;
+  const Fp8Out q8{(uint8_t*)q, scale, amax, parts, fmt};
+  switch ((cols + 511) / 512) {
+    case 1: return bwd_dispatch<1>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
+    case 2: return bwd_dispatch<2>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
+    case 3: case 4: return bwd_dispatch<4>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
+    default: return bwd_dispatch<8>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
   }
 }
 

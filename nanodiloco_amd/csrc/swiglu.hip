@@ -2,17 +2,21 @@
 //   fwd: act = silu(g) * u                      -> [n, F]
 //   bwd: dg = dy * u * s * (1 + g * (1 - s)),  du = dy * silu(g)   -> d(gu) [n, 2F]
 // Memory-bound; 8 elements per thread with 16-B bf16 vector accesses, fp32 math.
+// Q: fused fp8 side output for the fp8 inner step (common.h Fp8Out): act8 = e4m3 of the activation
+// (the down projection's operand), d(gu)8 = e5m2 of the gradient (the gate|up dgrad operand),
+// written by the same pass instead of a separate cast over the bf16 tensor (3 B/elem -> 1 B/elem).
 #include "common.h"
 
 using namespace nd;
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
-template <int DT>
+template <int DT, bool Q = false>
 __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const void* __restrict__ gu, void* __restrict__ out,
-                                                         int64_t n, int F) {
+                                                         int64_t n, int F, Fp8Out q8) {
   const int f8 = F >> 3;
   const int64_t total = n * f8;
+  float amax = 0.f;
   for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < total; it += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = it / f8;
     const int c = (int)(it % f8) * 8;
@@ -22,14 +26,20 @@ __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const void* __restrict_
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = g[j] * sigm(g[j]) * u[j];
     Vec8<DT>::store(out, r * F + c, o);
+    if (Q) {
+      round_bf16x8(o);
+      fp8_put8(q8, r * F + c, o, amax);
+    }
   }
+  if (Q) block_amax_commit<256>(amax, q8.amax, q8.parts);
 }
 
-template <int DT>
+template <int DT, bool Q = false>
 __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const void* __restrict__ dy, const void* __restrict__ gu,
-                                                         void* __restrict__ dgu, int64_t n, int F) {
+                                                         void* __restrict__ dgu, int64_t n, int F, Fp8Out q8) {
   const int f8 = F >> 3;
   const int64_t total = n * f8;
+  float amax = 0.f;
   for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < total; it += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = it / f8;
     const int c = (int)(it % f8) * 8;
@@ -45,7 +55,14 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const void* __restrict_
     }
     Vec8<DT>::store(dgu, r * 2 * F + c, dg);
     Vec8<DT>::store(dgu, r * 2 * F + F + c, du);
+    if (Q) {
+      round_bf16x8(dg);
+      round_bf16x8(du);
+      fp8_put8(q8, r * 2 * F + c, dg, amax);
+      fp8_put8(q8, r * 2 * F + F + c, du, amax);
+    }
   }
+  if (Q) block_amax_commit<256>(amax, q8.amax, q8.parts);
 }
 
 static unsigned grid_for(int64_t total) {
@@ -56,15 +73,35 @@ static unsigned grid_for(int64_t total) {
 ND_API int nd_swiglu_fwd(const void* gu, void* out, int dt, int64_t n, int F, hipStream_t s) {
   if (F % 8) return (int)hipErrorInvalidValue;
   const unsigned g = grid_for(n * (F / 8));
-  if (dt == BF16) hipLaunchKernelGGL(swiglu_fwd_kernel<BF16>, dim3(g), dim3(256), 0, s, gu, out, n, F);
-  else hipLaunchKernelGGL(swiglu_fwd_kernel<F32>, dim3(g), dim3(256), 0, s, gu, out, n, F);
+  const Fp8Out none{nullptr, nullptr, nullptr, 1, 0};
+  if (dt == BF16) hipLaunchKernelGGL(swiglu_fwd_kernel<BF16>, dim3(g), dim3(256), 0, s, gu, out, n, F, none);
+  else hipLaunchKernelGGL(swiglu_fwd_kernel<F32>, dim3(g), dim3(256), 0, s, gu, out, n, F, none);
   ND_LAUNCH_CHECK();
 }
 
 ND_API int nd_swiglu_bwd(const void* dy, const void* gu, void* dgu, int dt, int64_t n, int F, hipStream_t s) {
   if (F % 8) return (int)hipErrorInvalidValue;
   const unsigned g = grid_for(n * (F / 8));
-  if (dt == BF16) hipLaunchKernelGGL(swiglu_bwd_kernel<BF16>, dim3(g), dim3(256), 0, s, dy, gu, dgu, n, F);
-  else hipLaunchKernelGGL(swiglu_bwd_kernel<F32>, dim3(g), dim3(256), 0, s, dy, gu, dgu, n, F);
+  const Fp8Out none{nullptr, nullptr, nullptr, 1, 0};
+  if (dt == BF16) hipLaunchKernelGGL(swiglu_bwd_kernel<BF16>, dim3(g), dim3(256), 0, s, dy, gu, dgu, n, F, none);
+  else hipLaunchKernelGGL(swiglu_bwd_kernel<F32>, dim3(g), dim3(256), 0, s, dy, gu, dgu, n, F, none);
+  ND_LAUNCH_CHECK();
+}
+
+// bf16 variants with the fused fp8 side output (q: [n, F] fwd / [n, 2F] bwd fp8 bytes)
+ND_API int nd_swiglu_fwd_q(const void* gu, void* out, int64_t n, int F, void* q, const float* scale, float* amax,
+                           int parts, int fmt, hipStream_t s) {
+  if (F % 8 || !q || !scale || !amax || parts < 1) return (int)hipErrorInvalidValue;
+  const Fp8Out q8{(uint8_t*)q, scale, amax, parts, fmt};
+  hipLaunchKernelGGL((swiglu_fwd_kernel<BF16, true>), dim3(grid_for(n * (F / 8))), dim3(256), 0, s, gu, out, n, F, q8);
+  ND_LAUNCH_CHECK();
+}
+
+ND_API int nd_swiglu_bwd_q(const void* dy, const void* gu, void* dgu, int64_t n, int F, void* q, const float* scale,
+                           float* amax, int parts, int fmt, hipStream_t s) {
+  if (F % 8 || !q || !scale || !amax || parts < 1) return (int)hipErrorInvalidValue;
+  const Fp8Out q8{(uint8_t*)q, scale, amax, parts, fmt};
+  hipLaunchKernelGGL((swiglu_bwd_kernel<BF16, true>), dim3(grid_for(n * (F / 8))), dim3(256), 0, s, dy, gu, dgu, n, F,
+                     q8);
   ND_LAUNCH_CHECK();
 }

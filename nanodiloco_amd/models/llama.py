@@ -161,28 +161,39 @@ class LlamaForCausalLM:
                 ops.transpose_into(e[0], e[2])
                 e[1] = self.store.version
 
-    def _linear(self, key, x, w, gw):
+    def _linear(self, key, x, w, gw, x8=None):
         if self.fp8 is not None:
-            return self.fp8(key, x, w, gw, self.store.version)
+            return self.fp8(key, x, w, gw, self.store.version, x8)
         return ops.linear(x, w, gw, self._wt(key, w))
 
-    def _layer(self, i, h, y, cos, sin, B, T, next_norm):
+    def _q8(self, key: str, grad: bool = False):
+        """fp8 inner step: fused-producer quantisation target for projection ``key``'s input
+        (``grad=False``) or output gradient (``grad=True``); None when not applicable."""
+        if self.fp8 is None or not self.training or not torch.is_grad_enabled():
+            return None
+        return self.fp8.dy_target(key) if grad else self.fp8.x_target(key)
+
+    def _layer(self, i, h, y, cos, sin, B, T, next_norm, y8=None):
         c = self.config
         p = f"model.layers.{i}."
         cdt = self.compute_dtype
         eps = c.rms_norm_eps
         qn = self._qkv_names[i]
-        qkv = self._linear(f"{i}.qkv", y, self._fused(qn, "shadow"), self._fused(qn, "grad"))
+        qkv = self._linear(f"{i}.qkv", y, self._fused(qn, "shadow"), self._fused(qn, "grad"), y8)
         o = ops.attention(qkv, cos, sin, B, T, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
                           inplace=True)
         a = self._linear(f"{i}.o", o, self._w(p + "self_attn.o_proj.weight"), self._g(p + "self_attn.o_proj.weight"))
+        q_gu = self._q8(f"{i}.gu")
         y, h = ops.add_rmsnorm(h, a, self._m(p + "post_attention_layernorm.weight"),
-                               self._g(p + "post_attention_layernorm.weight"), eps, cdt)
+                               self._g(p + "post_attention_layernorm.weight"), eps, cdt,
+                               q8=q_gu, q8_bwd=self._q8(f"{i}.o", grad=True))
         gn = self._gu_names[i]
-        gu = self._linear(f"{i}.gu", y, self._fused(gn, "shadow"), self._fused(gn, "grad"))
-        act = ops.swiglu(gu)
+        gu = self._linear(f"{i}.gu", y, self._fused(gn, "shadow"), self._fused(gn, "grad"),
+                          q_gu.out if q_gu is not None else None)
+        q_down = self._q8(f"{i}.down")
+        act = ops.swiglu(gu, q8=q_down, q8_bwd=self._q8(f"{i}.gu", grad=True))
         m = self._linear(f"{i}.down", act, self._w(p + "mlp.down_proj.weight"),
-                         self._g(p + "mlp.down_proj.weight"))
+                         self._g(p + "mlp.down_proj.weight"), q_down.out if q_down is not None else None)
         return m, h
 
     def hidden_states(self, input_ids: torch.Tensor) -> torch.Tensor:
@@ -193,19 +204,24 @@ class LlamaForCausalLM:
         eps = c.rms_norm_eps
         cos, sin = ops.rope_cache(T, c.head_dim, c.rope_theta, c.rope_scaling, self.device)
         h = ops.embedding(input_ids, self._m("model.embed_tokens.weight"), self._g("model.embed_tokens.weight"))
+        q = self._q8("0.qkv")
         y = ops.rmsnorm(h, self._m("model.layers.0.input_layernorm.weight"),
-                        self._g("model.layers.0.input_layernorm.weight"), eps, cdt)
+                        self._g("model.layers.0.input_layernorm.weight"), eps, cdt, q8=q)
+        y8 = q.out if q is not None else None
         L = c.num_hidden_layers
         for i in range(L):
             nxt = f"model.layers.{i + 1}.input_layernorm.weight" if i + 1 < L else "model.norm.weight"
             if self.activation_checkpointing and self.training and torch.is_grad_enabled():
                 from torch.utils.checkpoint import checkpoint
-                m, h = checkpoint(self._layer, i, h, y, cos, sin, B, T, nxt, use_reentrant=False)
+                m, h = checkpoint(self._layer, i, h, y, cos, sin, B, T, nxt, None, use_reentrant=False)
             else:
-                m, h = self._layer(i, h, y, cos, sin, B, T, nxt)
+                m, h = self._layer(i, h, y, cos, sin, B, T, nxt, y8)
             if self.layer_hook is not None and torch.is_grad_enabled():
                 h = _GradHook.apply(h, self.layer_hook, i)
-            y, h = ops.add_rmsnorm(h, m, self._m(nxt), self._g(nxt), eps, cdt)
+            q = self._q8(f"{i + 1}.qkv") if i + 1 < L else None
+            y, h = ops.add_rmsnorm(h, m, self._m(nxt), self._g(nxt), eps, cdt, q8=q,
+                                   q8_bwd=self._q8(f"{i}.down", grad=True))
+            y8 = q.out if q is not None else None
         return y
 
     def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None, attention_mask=None,

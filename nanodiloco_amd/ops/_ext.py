@@ -130,6 +130,8 @@ def _declare(L: ctypes.CDLL):
         "nd_rmsnorm_fwd": [P, I, P, I, P, P, I, P, P, L64, I, F, P],
         "nd_rmsnorm_bwd": [P, I, P, P, P, P, P, I, P, L64, I, P, P],
         "nd_colsum_add": [P, P, I, I, P],
+        "nd_rmsnorm_fwd_q": [P, I, P, I, P, P, I, P, P, L64, I, F, P, P, P, I, I, P],
+        "nd_rmsnorm_bwd_q": [P, I, P, P, P, P, P, I, P, L64, I, P, P, P, P, I, I, P],
         "nd_transpose_bf16": [P, P, I, I, L64, L64, P],
         # rope (in place on packed qkv)
         "nd_rope_inplace": [P, I, P, P, L64, I, I, I, I, I, I, P],
@@ -140,6 +142,8 @@ def _declare(L: ctypes.CDLL):
         # mlp
         "nd_swiglu_fwd": [P, P, I, L64, I, P],
         "nd_swiglu_bwd": [P, P, P, I, L64, I, P],
+        "nd_swiglu_fwd_q": [P, P, L64, I, P, P, P, I, I, P],
+        "nd_swiglu_bwd_q": [P, P, P, L64, I, P, P, P, I, I, P],
         # loss
         "nd_ce_fwd_bwd": [P, I, P, P, P, L64, I, I, P, P, F, P],
         # embedding

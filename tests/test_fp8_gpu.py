@@ -55,6 +55,19 @@ def test_cast_t_matches_torch(fmt, dt):
     assert torch.equal(qt2.view(torch.uint8), ref2.t().contiguous().view(torch.uint8))
 
 
+@pytest.mark.parametrize("shape", [(1024, 2688), (96, 72)])
+def test_fp8_weight_current_scaling(shape):
+    """Fp8Weight: amax-only pass + one cast/transpose pass == torch current scaling of W and W^T."""
+    w = (torch.randn(*shape, device="cuda") * 0.02).bfloat16()
+    wq = fp8.Fp8Weight().get(w, version=0)
+    s = fp8.FMAX[fp8.E4M3] / w.float().abs().max()
+    ref = (w.float() * s).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert torch.allclose(wq.inv, (1.0 / s).reshape(1))
+    assert torch.equal(wq.w8.view(torch.uint8), ref.view(torch.uint8))
+    assert torch.equal(wq.wT8.view(torch.uint8), ref.t().contiguous().view(torch.uint8))
+    assert wq.get(w, version=0) is wq and wq.version == 0
+
+
 @pytest.mark.parametrize("wgrad_fp8", [True, False])
 def test_fp8_linear_close_to_fp32(wgrad_fp8):
     M, N, K = 2048, 1536, 1024
@@ -99,3 +112,90 @@ def test_fp8_training_tracks_bf16():
     b, f = losses[False], losses[True]
     assert f[-1] < 0.5 * f[0], f  # fp8 model memorises the batch
     assert abs(f[-1] - b[-1]) < 0.15 * b[0], (b[-1], f[-1])
+
+
+# ----------------------------------------------------------------- fused producer-side quantisation
+def _target(fmt, scale=23.0):
+    r = fp8.Fp8Recipe("cuda", capacity=4)
+    k = r.new_slot(fmt)
+    r.scale[k] = scale
+    r.ready[k] = True
+    return r, k, r.target(k, fmt)
+
+
+@pytest.mark.parametrize("fmt", [fp8.E4M3, fp8.E5M2])
+def test_fused_swiglu_quant_bitwise(fmt):
+    """SwiGLU fwd/bwd fp8 side outputs == a separate cast of the bf16 outputs (bytes and amax)."""
+    from nanodiloco_amd.ops.swiglu import SwiGLUFn
+    gu = torch.randn(300, 2 * 2688, device="cuda").bfloat16().requires_grad_(True)
+    r, k, q = _target(fmt)
+    rb, kb, qb = _target(fp8.E5M2, 3.0)
+    out = SwiGLUFn.apply(gu, q, qb)
+    ref = fp8.cast(out.detach(), r.scale[k:k + 1], fmt)
+    assert torch.equal(q.out.view(torch.uint8), ref.view(torch.uint8))
+    assert r.amax[k].max().item() == out.detach().float().abs().max().item()
+    dy = torch.randn_like(out)
+    (dgu,) = torch.autograd.grad(out, gu, dy)
+    q8 = rb.take_stashed(kb, dgu)
+    assert q8 is not None
+    refb = fp8.cast(dgu, rb.scale[kb:kb + 1], fp8.E5M2)
+    assert torch.equal(q8.view(torch.uint8), refb.view(torch.uint8))
+    assert rb.amax[kb].max().item() == dgu.float().abs().max().item()
+
+
+@pytest.mark.parametrize("residual", [False, True])
+def test_fused_rmsnorm_quant_bitwise(residual):
+    """RMSNorm fwd (y -> e4m3) and bwd (branch grad -> e5m2) fp8 side outputs == separate casts."""
+    rows, cols = 777, 1024
+    h = torch.randn(rows, cols, device="cuda")
+    a = torch.randn(rows, cols, device="cuda").bfloat16()
+    w = 1 + 0.1 * torch.randn(cols, device="cuda")
+    r, k, q = _target(fp8.E4M3, 50.0)
+    rb, kb, qb = _target(fp8.E5M2, 1000.0)
+    hr = h.clone().requires_grad_(True)
+    ar = a.clone().requires_grad_(True)
+    if residual:
+        y, hn = ops.add_rmsnorm(hr, ar, w, None, 1e-5, torch.bfloat16, q8=q, q8_bwd=qb)
+    else:
+        y = ops.rmsnorm(hr, w, None, 1e-5, torch.bfloat16, q8=q)
+    ref = fp8.cast(y.detach(), r.scale[k:k + 1], fp8.E4M3)
+    assert torch.equal(q.out.view(torch.uint8), ref.view(torch.uint8))
+    assert r.amax[k].max().item() == y.detach().float().abs().max().item()
+    if residual:
+        dy = torch.randn_like(y)
+        (da,) = torch.autograd.grad(y, ar, dy)
+        q8 = rb.take_stashed(kb, da)
+        assert q8 is not None
+        refb = fp8.cast(da, rb.scale[kb:kb + 1], fp8.E5M2)
+        assert torch.equal(q8.view(torch.uint8), refb.view(torch.uint8))
+
+
+def test_fused_quant_training_matches_separate_casts():
+    """The fp8 model trains identically with producer-fused and with separate operand casts."""
+    cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                                     num_hidden_layers=2, vocab_size=1000))
+    batches = [torch.randint(0, 1000, (4, 256), device="cuda") for _ in range(6)]
+
+    def run(fused):
+        fp8.set_fused_quant(fused)
+        try:
+            m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16, fp8=True).init_weights(2)
+            opt = FlatAdamW(m.store, lr=1e-3)
+            losses = []
+            for i, ids in enumerate(batches):
+                out = m(ids, labels=ids, loss_scale=0.5)
+                out.loss.backward()
+                losses.append(out.loss.detach())
+                if i % 2 == 1:
+                    opt.step()
+                    opt.zero_grad()
+                    m.fp8.recipe.update()
+            torch.cuda.synchronize()
+            return torch.stack(losses).cpu(), m.store.master.clone()
+        finally:
+            fp8.set_fused_quant(True)
+
+    l0, p0 = run(False)
+    l1, p1 = run(True)
+    assert (l1 - l0).abs().max().item() < 2e-3, (l0, l1)
+    assert ((p1 - p0).norm() / p0.norm()).item() < 1e-3
