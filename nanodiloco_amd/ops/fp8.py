@@ -17,7 +17,8 @@ Recipe (per-tensor scaling, the common "delayed scaling" scheme):
 * fused operand quantisation: once a slot's scale exists (delayed scaling: known before the
   producer runs), the PRODUCER of an operand writes its fp8 copy in the same pass as its bf16
   output (``QuantTarget``): RMSNorm forward -> x of q|k|v and gate|up, SwiGLU forward -> x of down,
-  SwiGLU backward -> dy of gate|up, RMSNorm backward -> dy of o and down.  The backward side
+  SwiGLU backward -> dy of gate|up, RMSNorm backward -> dy of o and down.  (The attention
+  epilogues stay plain: their fused variants cost occupancy -- measured -2.6 % end to end.)  The backward side
   reaches the consuming ``Fp8LinearFn.backward`` through ``Fp8Recipe.stash`` (keyed by slot, checked
   against the gradient tensor's storage).  Bitwise the separate cast over the bf16 tensor.
 """
