@@ -113,7 +113,7 @@ def _rel(a, b):
     return ((a - b).float().norm() / b.float().norm()).item()
 
 
-def _schedule_check(cfg, batches, graphed, switch):
+def _schedule_check(cfg, batches, graphed, switch, floor_g=1e-3, floor_p=1e-4, floor_l=2e-4):
     """Run the reference schedule twice (its own run-to-run spread: hipBLASLt stream-K GEMMs and the
     embedding's float atomics are not bitwise reproducible) and the switched schedule once; the
     switched run must sit within a small multiple of that spread."""
@@ -127,9 +127,9 @@ def _schedule_check(cfg, batches, graphed, switch):
         switch(False)
     # floors at bf16-rounding level: a read of a half-written gradient moves the affected weights by
     # ~lr in a wrong direction (>= 1e-2 relative on them), far above these
-    tol_g = max(4 * _rel(g0b, g0), 1e-3)
-    tol_p = max(4 * _rel(p0b, p0), 1e-4)
-    tol_l = max(4 * (l0b - l0).abs().max().item(), 2e-4)
+    tol_g = max(4 * _rel(g0b, g0), floor_g)
+    tol_p = max(4 * _rel(p0b, p0), floor_p)
+    tol_l = max(4 * (l0b - l0).abs().max().item(), floor_l)
     assert (l1 - l0).abs().max().item() <= tol_l, (l0, l0b, l1)
     assert _rel(g1, g0) <= tol_g, (_rel(g1, g0), _rel(g0b, g0))
     assert _rel(p1, p0) <= tol_p, (_rel(p1, p0), _rel(p0b, p0))
@@ -147,7 +147,10 @@ def test_wgrad_overlap_matches_serial(graphed):
     ops.set_backend("hip")
     cfg = LlamaConfig.from_dict(_CFG_SMALL)
     batches = [torch.randint(0, 1000, (4, 256), device="cuda") for _ in range(6)]
-    _schedule_check(cfg, batches, graphed, ops.set_wgrad_overlap)
+    # bf16-ulp floors: hipBLASLt's stream-K GEMMs co-running with the side stream combine their
+    # partial tiles in a timing-dependent order (1 bf16 ulp on some outputs -> ~1e-3 on grads);
+    # serial runs reproduce bitwise.  A missing join is >= 1e-2.
+    _schedule_check(cfg, batches, graphed, ops.set_wgrad_overlap, floor_g=5e-3, floor_p=5e-4, floor_l=1e-3)
 
 
 @pytest.mark.parametrize("graphed", [False, True])
