@@ -70,6 +70,8 @@ def parse():
                          "default: beside hipBLASLt's stream-K GEMMs it stalls (docs/DESIGN.md)")
     ap.add_argument("--wgrad-variant", default=None,
                     help="ND_WGRAD_VARIANT for the weight-gradient kernel (A/B of kernel schedules)")
+    ap.add_argument("--attn-fused-stats", type=int, default=1, choices=[0, 1],
+                    help="attention backward: row statistics inside the dQ kernel (0: separate passes)")
     ap.add_argument("--dgrad-t", type=int, default=1, choices=[0, 1],
                     help="input-gradient GEMMs on transposed weight copies (K-contiguous NT layout)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
@@ -85,6 +87,7 @@ def main():
     ops.set_backend(a.ops)
     ops.set_wgrad_overlap(a.wgrad_overlap)
     ops.set_dgrad_transposed(bool(a.dgrad_t))
+    ops.set_attn_fused_stats(bool(a.attn_fused_stats))
     if a.fp8:
         from nanodiloco_amd.ops import fp8 as _fp8
         _fp8.set_fused_quant(bool(a.fp8_fused_quant))

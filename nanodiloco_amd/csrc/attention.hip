@@ -482,13 +482,20 @@ __global__ void __launch_bounds__(256) attn_bwd_pre_kernel(const bf16_t* __restr
 }
 
 // dQ: per 128 queries of one (b, head), streaming 64-key K/V tiles up to the diagonal.
-template <int HD, bool ROPE, bool ROPE_OUT, bool DMA = false>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
+// PRE: the backward's row statistics are produced here instead of by attn_bwd_pre_kernel +
+// attn_neg_stats_kernel: each lane already holds half of its query's dO row, so it loads the same
+// half of O, dots, and one lane^32 exchange gives delta = rowsum(dO * O); the kernel then writes
+// -delta and -LSE/c (the seeds of the dK/dV kernel, which therefore runs after this one).
+template <int HD, bool ROPE, bool ROPE_OUT, bool DMA = false, bool PRE = false>  // DMA: LDS-DMA K/V staging
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                              const bf16_t* __restrict__ V, const bf16_t* __restrict__ dO,
                                                              const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                              bf16_t* __restrict__ dQ, int B, int nh, int nkv, int T,
                                                              int64_t ld, int64_t ldo, float scale,
-                                                             const float* __restrict__ cosT, const float* __restrict__ sinT) {
+                                                             const float* __restrict__ cosT, const float* __restrict__ sinT,
+                                                             const bf16_t* __restrict__ O = nullptr,
+                                                             float* __restrict__ NL = nullptr,
+                                                             float* __restrict__ ND = nullptr) {
   constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * BN * HD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * BN * HD];
@@ -515,7 +522,26 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
   if (ROPE && qi < T) rope_frags<HD>(qf, cosT, sinT, qi, h);
   const int64_t rowstat = ((int64_t)b * nh + head) * T;
   const float lse = qi < T ? LSE[rowstat + qi] : 0.f;
-  const float dlt = qi < T ? DELTA[rowstat + qi] : 0.f;
+  float dlt;
+  if constexpr (PRE) {
+    float acc = 0.f;
+    if (qi < T) {
+      const bf16_t* Orow = O + ((int64_t)b * T + qi) * ldo + (int64_t)head * HD;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const bf16x8 of = load16(Orow + 16 * t + 8 * h);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc = fmaf(bf2f((bf16_t)of[j]), bf2f((bf16_t)dof[t][j]), acc);
+      }
+    }
+    dlt = acc + __shfl_xor(acc, 32, 64);
+    if (qi < T && h == 0) {
+      ND[rowstat + qi] = -dlt;
+      NL[rowstat + qi] = -lse * (1.f / c);
+    }
+  } else {
+    dlt = qi < T ? DELTA[rowstat + qi] : 0.f;
+  }
   f32x16 dq[NO];
 #pragma unroll
   for (int o = 0; o < NO; ++o) dq[o] = f32x16{};
@@ -1035,6 +1061,51 @@ ND_API int nd_attn_bwd(const void* q, const void* k, const void* v, const void* 
     case 32: return bwd_launch<32>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
     case 64: return bwd_launch<64>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
     case 128: return bwd_launch<128>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// Backward with the row statistics fused into the dQ kernel (PRE): dQ (writes -delta, -LSE/c into
+// ws) -> dK/dV; no attn_bwd_pre / attn_neg_stats passes.  LDS-DMA kernels only: q/k already rotated
+// (rope_mode 0 or 2), T % 64 == 0.  ws: 2 * B * nh * T floats.
+template <int HD, bool ROPE_OUT>
+static int bwd_fused_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                            const float* lse, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T,
+                            int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, hipStream_t s) {
+  const int nb = (T + 127) / 128;
+  const int64_t n = (int64_t)B * nh * T;
+  float *nl = ws, *nd = ws + n;
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, ROPE_OUT, true, true>), dim3(nb * B * nh), dim3(256), 0, s,
+                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
+                     (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd);
+  if (T % 128 == 0)
+    hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128>), dim3(nb * B * nkv), dim3(256), 0, s,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
+                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+  else
+    hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
+                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+  ND_LAUNCH_CHECK();
+}
+
+ND_API int nd_attn_bwd_fused(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                             const float* lse, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T,
+                             int hd, int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale,
+                             int rope_mode, hipStream_t s) {
+  if (nh % nkv || (ld % 8) || (ldo % 8) || T % 64 || ws == nullptr || rope_mode == 1) return (int)hipErrorInvalidValue;
+  if (rope_mode == 2 && !(cosT && sinT)) return (int)hipErrorInvalidValue;
+  switch (hd) {
+#define ND_BF(H)                                                                                               \
+  case H:                                                                                                      \
+    return rope_mode == 2 ? bwd_fused_launch<H, true>(q, k, v, o, dout, lse, dq, dk, dv, ws, B, nh, nkv, T, ld, \
+                                                      ldo, cosT, sinT, scale, s)                               \
+                          : bwd_fused_launch<H, false>(q, k, v, o, dout, lse, dq, dk, dv, ws, B, nh, nkv, T, ld, \
+                                                       ldo, cosT, sinT, scale, s);
+    ND_BF(32)
+    ND_BF(64)
+    ND_BF(128)
+#undef ND_BF
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -139,6 +139,7 @@ def _declare(L: ctypes.CDLL):
         "nd_attn_fwd": [P, P, P, P, P, I, I, I, I, I, L64, L64, P, P, F, P],
         "nd_attn_bwd_pre": [P, P, P, I, I, I, L64, L64, P],
         "nd_attn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, L64, L64, P, P, F, I, P],
+        "nd_attn_bwd_fused": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, L64, L64, P, P, F, I, P],
         # mlp
         "nd_swiglu_fwd": [P, P, I, L64, I, P],
         "nd_swiglu_bwd": [P, P, P, I, L64, I, P],

@@ -8,8 +8,9 @@ write ``O`` as ``[B*T, nh*hd]`` -- exactly the o_proj GEMM input.
 HIP path (RoPE: q|k rotated in place by one streaming pass -- no copy; dq/dk are un-rotated inside the
 backward kernels' store epilogues, so the backward needs no extra pass)
   fwd: ``nd_rope_inplace`` then ``nd_attn_fwd``  -- MFMA flash attention, online softmax, saves LSE (fp32, log2 domain)
-  bwd: ``nd_attn_bwd_pre`` (delta = rowsum(dO * O)), ``nd_attn_bwd`` = a key-parallel dK/dV kernel
-       and a query-parallel dQ kernel (both recompute P from LSE; no atomics -> deterministic).
+  bwd: ``nd_attn_bwd_fused`` = a query-parallel dQ kernel that also computes delta = rowsum(dO * O)
+       and the dK/dV kernel's seeds, then a key-parallel dK/dV kernel (both recompute P from LSE; no
+       atomics -> deterministic); ``nd_attn_bwd_pre`` + ``nd_attn_bwd`` is the unfused form.
 ``nd_rope_inplace`` (stand-alone rotation kernel) remains available for other callers.
 GQA (nkv < nh) is handled by head-index mapping inside the kernels (no K/V repetition).
 """
@@ -42,6 +43,15 @@ def _rope(qkv, cos, sin, B, T, nh, nkv, hd, inverse):
                "nd_rope_inplace")
 
 
+_FUSED_STATS = {"enabled": True}
+
+
+def set_attn_fused_stats(enabled: bool) -> None:
+    """Backward row statistics computed inside the dQ kernel (default) vs the separate
+    delta / statistics kernels (A/B)."""
+    _FUSED_STATS["enabled"] = bool(enabled)
+
+
 class FlashAttnFn(torch.autograd.Function):
     """RoPE is applied to q|k IN PLACE in the packed projection output (one streaming pass, no copy):
     that buffer is this op's private input -- the projection's backward saved its input, not its
@@ -72,6 +82,17 @@ class FlashAttnFn(torch.autograd.Function):
         ld = qkv.shape[1]
         L = _ext.lib()
         dev = do.device
+        if _FUSED_STATS["enabled"] and T % 64 == 0:
+            # dQ kernel computes delta = rowsum(dO * O) itself and seeds the dK/dV kernel
+            dqkv = torch.empty_like(qkv)
+            k, v = qkv[:, nh * hd:], qkv[:, (nh + nkv) * hd:]
+            dk, dv = dqkv[:, nh * hd:], dqkv[:, (nh + nkv) * hd:]
+            ws = torch.empty(2, B, nh, T, dtype=torch.float32, device=dev)
+            _ext.check(L.nd_attn_bwd_fused(_ext.ptr(qkv), _ext.ptr(k), _ext.ptr(v), _ext.ptr(o), _ext.ptr(do),
+                                           _ext.ptr(lse), _ext.ptr(dqkv), _ext.ptr(dk), _ext.ptr(dv), _ext.ptr(ws),
+                                           B, nh, nkv, T, hd, ld, nh * hd, _ext.ptr(cos), _ext.ptr(sin),
+                                           float(hd ** -0.5), 2, _ext.stream_ptr(dev)), "nd_attn_bwd_fused")
+            return dqkv, None, None, None, None, None, None, None
         delta = torch.empty(B, nh, T, dtype=torch.float32, device=dev)
         _ext.check(L.nd_attn_bwd_pre(_ext.ptr(o), _ext.ptr(do), _ext.ptr(delta), B, nh, T, hd, nh * hd,
                                      _ext.stream_ptr(dev)), "nd_attn_bwd_pre")

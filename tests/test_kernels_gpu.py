@@ -334,3 +334,26 @@ def test_colsum_add(rows):
     ref_ = out.double() + part.double().sum(0)
     _ext.check(_ext.lib().nd_colsum_add(part.data_ptr(), out.data_ptr(), rows, cols, _ext.stream_ptr()), "colsum")
     assert rel(out, ref_) < 1e-6
+
+
+
+@pytest.mark.parametrize("kv", [16, 4])
+def test_attention_bwd_fused_stats_matches_separate(kv):
+    """Row statistics computed inside the dQ kernel == the separate delta/statistics passes (up to
+    the order of the delta summation), with GQA too."""
+    from nanodiloco_amd.ops.attention import rope_cache, set_attn_fused_stats
+    B, T, nh, hd = 2, 512, 16, 64
+    qkv = (torch.randn(B * T, (nh + 2 * kv) * hd, device=DEV) * 0.5).bfloat16()
+    cos, sin = rope_cache(T, hd, 10000.0, None, DEV)
+    do = torch.randn(B * T, nh * hd, device=DEV).bfloat16()
+    grads = []
+    for fused in (False, True):
+        set_attn_fused_stats(fused)
+        try:
+            x = qkv.clone().requires_grad_(True)
+            o = ops.attention(x, cos, sin, B, T, nh, kv, hd)
+            (g,) = torch.autograd.grad(o, x, do)
+            grads.append(g.float())
+        finally:
+            set_attn_fused_stats(True)
+    assert rel(grads[1], grads[0]) < 2e-3
