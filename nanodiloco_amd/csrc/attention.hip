@@ -208,6 +208,19 @@ __device__ __forceinline__ void load_tile(S& st, const bf16_t* base, int64_t str
 
 constexpr float LOG2E = 1.4426950408889634f;
 
+// x (op) x[lane ^ 32] with one v_permlane32_swap_b32 (gfx950) instead of __shfl_xor's LDS round
+// trip (ds_bpermute + lgkmcnt wait).  With both operands = x the swap returns {x[lane & 31],
+// x[32 + (lane & 31)]}: the pair's two values in the same order on both halves, so max and sum
+// come out bitwise identical in lane l and l ^ 32.
+__device__ __forceinline__ float pair_max32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair_sum32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // Raw v_exp_f32 (no denormal range fix-up: exp2f lowers to ~6 extra VALU ops per call).  Inputs
 // here are <= 0 (scores minus a running max / LSE); results below 2^-126 flush to 0, harmless for P.
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -403,7 +416,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;  // raw-score max -> log2 domain (c > 0)
+      mx = pair_max32(mx) * c;  // raw-score max -> log2 domain (c > 0)
       const float mnew = fmaxf(m, mx);
       const float alpha = fexp2(m - mnew);
       m = mnew;
@@ -443,7 +456,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
       }
     }
   }
-  const float lt = l + __shfl_xor(l, 32, 64);
+  const float lt = pair_sum32(l);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   if (qi < T) {
     store_T<HD>(O + ((int64_t)b * T + qi) * ldo + (int64_t)head * HD, oacc, inv, h, nullptr, nullptr, 0);
@@ -534,7 +547,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
         for (int j = 0; j < 8; ++j) acc = fmaf(bf2f((bf16_t)of[j]), bf2f((bf16_t)dof[t][j]), acc);
       }
     }
-    dlt = acc + __shfl_xor(acc, 32, 64);
+    dlt = pair_sum32(acc);
     if (qi < T && h == 0) {
       ND[rowstat + qi] = -dlt;
       NL[rowstat + qi] = -lse * (1.f / c);
