@@ -347,9 +347,7 @@ __device__ __forceinline__ void reg_tile(bf16_t* tile, const bf16_t* base, int64
 }
 }  // namespace
 
-// PRIO: 1 = s_setprio(1) around every 8-MFMA cluster (T5); 2 = static form: the second-dispatched wave
-// half (waves 4-7) runs at priority 1 for the whole kernel (cdna guide T5)
-template <bool SCHED, bool NODMA = false, int PRIO = 0>  // NODMA: diagnostic only (skips the loads)
+template <bool SCHED, bool NODMA = false>  // NODMA: diagnostic only (skips the loads; garbage result)
 __global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                            float* __restrict__ C, float* __restrict__ slab, int M,
                                                            int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
@@ -391,7 +389,6 @@ __global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restr
       reg_tile(tb, B, ldb, k0, kend, n0, N);
     }
   };
-  if (PRIO == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   if (nk > 0) stage(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -414,12 +411,10 @@ __global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restr
 #pragma unroll
         for (int a = 0; a < 4; ++a) fa[nxt][a] = frag2(a_t, (ks + 1) * 16, wm * 128 + a * 32, g, i16);
       }
-      if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(fa[cur][a], fb[cur][b], acc[a][b]);
-      if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
       if (SCHED && ks + 1 < BK3 / 16) {
         // interleave the 12 transposing reads of k-step ks+1 between the 8 MFMAs of k-step ks
 #pragma unroll
@@ -511,12 +506,13 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
   const int large = plan(M, N, K, &S);
   if (S > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
   // ND_WGRAD_VARIANT (A/B runs): "reg" register-staged 256 kernel, "dmas" LDS-DMA with the
-  // sched_group_barrier interleave, "p1"/"p2" setprio forms, "nodma" compute-only diagnostic (skips
-  // the loads: wrong result); default ("dma0"): LDS-DMA, compiler-scheduled.  (Measured and dropped, see docs/DESIGN.md: a 4-deep
+  // sched_group_barrier interleave, "nodma" compute-only diagnostic (skips the loads: wrong result);
+  // default ("dma0"): LDS-DMA, compiler-scheduled.  (s_setprio around the MFMA clusters, both
+  // per-cluster and the static waves-4-7 form, measured +-0 e2e and were dropped.)  (Measured and dropped, see docs/DESIGN.md: a 4-deep
   // BK=32 ring with counted vmcnt, a 16x16x32-MFMA version and a quadrant-phase pipeline -- all
   // 3-15 % slower than this kernel on the Llama-150M shapes.)
   const char* ev = getenv("ND_WGRAD_VARIANT");
-  const int variant = (ev && ev[0] == 'r') ? 1 : (ev && ev[0] == 'n') ? 4 : (ev && ev[0] == 'p') ? (ev[1] == '2' ? 6 : 5) : 0;
+  const int variant = (ev && ev[0] == 'r') ? 1 : (ev && ev[0] == 'n') ? 4 : 0;
   // the sched_group_barrier interleave (MFMA / 2 transposing reads) is opt-in ("dmas"): measured
   // 4-13 % SLOWER per kernel than the compiler's own schedule at 32k and 64k tokens, -1.7 % e2e
   const bool sched = ev && ev[0] == 'd' && ev[3] == 's';
@@ -537,20 +533,9 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
         (hipError_t)(hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_dma_kernel<true>),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) |
                      hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_dma_kernel<false>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) |
-                     hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_dma_kernel<false, false, 1>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) |
-                     hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_dma_kernel<false, false, 2>),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     (void)attr_ok;
-    if (variant == 5 || variant == 6) {  // "p1" / "p2": dma0 schedule + setprio forms (A/B)
-      if (variant == 5)
-        hipLaunchKernelGGL((wgrad_dma_kernel<false, false, 1>), dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A,
-                           (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
-      else
-        hipLaunchKernelGGL((wgrad_dma_kernel<false, false, 2>), dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A,
-                           (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
-    } else if (sched)
+    if (sched)
       hipLaunchKernelGGL(wgrad_dma_kernel<true>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A,
                          (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
     else
