@@ -43,3 +43,27 @@ def test_bench_two_ranks_share_gpu_gloo():
     assert j["outer_steps_in_window"] == 2  # H=2 inside a 4-step window
     assert j["ops"] == "hip" and j["dgrad_transposed"] is True
     assert j["value"] > 0 and j["final_loss"] == j["final_loss"]
+
+
+def test_trainer_two_workers_share_gpu_overlap_bf16_comm(tmp_path):
+    """CLI trainer, 2 DiLoCo workers on one GPU over gloo: overlapped outer step with bf16
+    pseudo-gradient transport and debug replica checks (the outer all-reduce result must be
+    bit-identical on both workers), plus a checkpoint that HF-style tooling can read."""
+    import os as _os
+    env = dict(os.environ, OMP_NUM_THREADS="4", PYTHONPATH=ROOT)
+    log = tmp_path / "log.jsonl"
+    ck = tmp_path / "ckpt"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "-m", "nanodiloco_amd",
+           "--llama-config-file", "configs/llama_tiny.json", "--batch-size", "8", "--per-device-batch-size", "4",
+           "--seq-length", "128", "--total-steps", "8", "--inner-steps", "4", "--warmup-steps", "2",
+           "--backend", "gloo", "--overlap-outer", "--comm-dtype", "bf16", "--debug-checks",
+           "--wandb", "off", "--log-file", str(log), "--log-every", "1", "--checkpoint-dir", str(ck)]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    recs = [json.loads(l) for l in open(log)]
+    assert recs and all(rec["loss"] == rec["loss"] for rec in recs if "loss" in rec)
+    assert any(rec.get("outer_step", 0) >= 1 for rec in recs)
+    files = set(_os.listdir(ck)) if ck.is_dir() else set()
+    found = files | {f for d in files if (ck / d).is_dir() for f in _os.listdir(ck / d)}
+    assert "model.safetensors" in found and "config.json" in found, found
