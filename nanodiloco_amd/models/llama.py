@@ -205,8 +205,10 @@ class LlamaForCausalLM:
         cos, sin = ops.rope_cache(T, c.head_dim, c.rope_theta, c.rope_scaling, self.device)
         h = ops.embedding(input_ids, self._m("model.embed_tokens.weight"), self._g("model.embed_tokens.weight"))
         q = self._q8("0.qkv")
-        y = ops.rmsnorm(h, self._m("model.layers.0.input_layernorm.weight"),
-                        self._g("model.layers.0.input_layernorm.weight"), eps, cdt, q8=q)
+        # (y, h): the embedding output feeds both the first norm and the residual stream; rmsnorm_res
+        # fuses the two gradient contributions inside the norm's backward kernel
+        y, h = ops.rmsnorm_res(h, self._m("model.layers.0.input_layernorm.weight"),
+                               self._g("model.layers.0.input_layernorm.weight"), eps, cdt, q8=q)
         y8 = q.out if q is not None else None
         L = c.num_hidden_layers
         for i in range(L):

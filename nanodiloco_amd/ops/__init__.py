@@ -3,7 +3,7 @@ PyTorch reference (``ops.reference``) for CPU tensors; see ``ops/_ext.py`` for t
 from ._ext import available as hip_available, set_backend, get_backend, ExtensionMissing
 from .linear import linear, wgrad_accumulate, set_wgrad_overlap, wgrad_overlap_enabled, join_wgrad, \
     set_dgrad_transposed, dgrad_transposed_enabled, transpose_into
-from .norm import rmsnorm, add_rmsnorm
+from .norm import rmsnorm, rmsnorm_res, add_rmsnorm
 from .embedding import embedding
 from .swiglu import swiglu
 from .attention import attention, rope_cache, set_attn_fused_stats
@@ -14,5 +14,5 @@ from . import reference
 __all__ = ["hip_available", "set_backend", "get_backend", "ExtensionMissing", "linear", "wgrad_accumulate",
            "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad",
            "set_dgrad_transposed", "dgrad_transposed_enabled", "transpose_into",
-           "rmsnorm", "add_rmsnorm", "set_attn_fused_stats", "embedding", "swiglu", "attention", "rope_cache", "lm_head_ce",
+           "rmsnorm", "rmsnorm_res", "add_rmsnorm", "set_attn_fused_stats", "embedding", "swiglu", "attention", "rope_cache", "lm_head_ce",
            "IGNORE_INDEX", "adamw_step", "global_grad_norm", "pseudograd", "outer_nesterov", "reference"]

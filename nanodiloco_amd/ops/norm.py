@@ -99,6 +99,43 @@ class RMSNormFn(torch.autograd.Function):
         return dx.to(x.dtype), None, None, None, None, None
 
 
+class RMSNormResFn(torch.autograd.Function):
+    """y = rmsnorm(x) * w, also returning x itself (as a view) for the residual stream.  Used for the
+    first norm, whose input (the embedding output) also starts the residual path: routing both uses
+    through this one node lets the backward kernel add the residual gradient (``dres``) in place of a
+    separate autograd accumulation, a full fp32 [N, d] read-read-write pass per micro-batch."""
+
+    @staticmethod
+    def forward(ctx, x, w, gw, eps, out_dtype, q8=None):
+        ctx.set_materialize_grads(False)
+        ctx.eps, ctx.gw, ctx.shape, ctx.y_dtype = eps, gw, x.shape, out_dtype
+        if _ext.use_hip(x):
+            y, hx, rstd = _hip_fwd(x.contiguous(), None, w, eps, out_dtype, q8)
+            ctx.save_for_backward(hx, w, rstd)
+            ctx.hip = True
+            return y.view(x.shape), x.view_as(x)
+        ctx.hip = False
+        ctx.save_for_backward(x, w)
+        return ref.rmsnorm(x.float(), w, eps).to(out_dtype), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        if dy is None:
+            dy = torch.zeros(ctx.shape, dtype=ctx.y_dtype, device=ctx.saved_tensors[0].device)
+        if ctx.hip:
+            hx, w, rstd = ctx.saved_tensors
+            dr = _rows(dres).float().contiguous() if dres is not None else None
+            dx, _ = _hip_bwd(dy, hx, w, rstd, dr, ctx.gw, None)
+            return dx.view(ctx.shape), None, None, None, None, None
+        x, w = ctx.saved_tensors
+        dx, dw = ref.rmsnorm_backward(dy, x, w, ctx.eps)
+        if dres is not None:
+            dx = dx + dres.float()
+        if ctx.gw is not None:
+            ctx.gw.add_(dw)
+        return dx.to(x.dtype), None, None, None, None, None
+
+
 class AddRMSNormFn(torch.autograd.Function):
     """h_new = h + a ; y = rmsnorm(h_new) * w.  Returns (y, h_new)."""
 
@@ -140,6 +177,12 @@ class AddRMSNormFn(torch.autograd.Function):
 def rmsnorm(x, w, gw, eps, out_dtype=None, q8=None):
     """``q8`` (fp8 inner step): fused fp8 copy of the output for the next projection (ops/fp8.py)."""
     return RMSNormFn.apply(x, w, gw, eps, out_dtype or x.dtype, q8)
+
+
+def rmsnorm_res(x, w, gw, eps, out_dtype=None, q8=None):
+    """(y, x): ``rmsnorm`` plus a pass-through of ``x`` whose gradient is fused into this op's
+    backward kernel; use when ``x`` also feeds the residual stream."""
+    return RMSNormResFn.apply(x, w, gw, eps, out_dtype or x.dtype, q8)
 
 
 def add_rmsnorm(h, a, w, gw, eps, out_dtype=None, q8=None, q8_bwd=None):

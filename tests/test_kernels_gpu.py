@@ -59,6 +59,28 @@ def test_rmsnorm_fwd_bwd(cols, residual):
         assert rel(ax.grad, ar.grad) < 1e-2
 
 
+def test_rmsnorm_res_fused_residual_grad():
+    """rmsnorm_res: the residual gradient enters the HIP backward kernel as ``dres``; compare with the
+    plain fp32 PyTorch reference where autograd sums the two uses of x."""
+    rows, cols, eps = 1000, 1024, 1e-5
+    x = torch.randn(rows, cols, device=DEV)
+    w = 1 + 0.1 * torch.randn(cols, device=DEV)
+    up = torch.randn(rows, cols, device=DEV).bfloat16()
+    ur = torch.randn(rows, cols, device=DEV)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = wr * (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + eps))
+    ((yr * up.float()).sum() + (xr * ur).sum()).backward()
+    xx = x.clone().requires_grad_(True)
+    gw = torch.zeros(cols, device=DEV)
+    y, h = ops.rmsnorm_res(xx, w, gw, eps, torch.bfloat16)
+    assert y.dtype == torch.bfloat16 and h.data_ptr() == xx.data_ptr()
+    ((y.float() * up.float()).sum() + (h * ur).sum()).backward()
+    assert rel(y, yr) < 5e-3
+    assert rel(xx.grad, xr.grad) < 1e-2
+    assert rel(gw, wr.grad) < 1e-2
+
+
 # ----------------------------------------------------------------------------------- rope
 @pytest.mark.parametrize("hd,nh,nkv", [(64, 4, 4), (128, 4, 2), (32, 4, 1)])
 def test_rope_inplace_matches_reference(hd, nh, nkv, hip_lib):

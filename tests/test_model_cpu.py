@@ -78,3 +78,32 @@ def test_activation_checkpointing_same_grads():
     m2 = LlamaForCausalLM(c, activation_checkpointing=True).init_weights(0)
     m2(ids, labels=ids).loss.backward()
     assert torch.allclose(m1.store.grad, m2.store.grad, atol=1e-7)
+
+
+def test_rmsnorm_res_fuses_residual_grad():
+    """ops.rmsnorm_res(x) == (rmsnorm(x), x) with the residual gradient summed inside the node."""
+    from nanodiloco_amd import ops
+    torch.manual_seed(0)
+    x = torch.randn(6, 32, dtype=torch.float64)
+    w = torch.randn(32, dtype=torch.float64)
+    up = torch.randn(6, 32, dtype=torch.float64)
+    ur = torch.randn(6, 32, dtype=torch.float64)
+    outs = []
+    for fused in (True, False):
+        xx = x.clone().requires_grad_(True)
+        gw = torch.zeros_like(w)
+        if fused:
+            y, h = ops.rmsnorm_res(xx, w, gw, 1e-5)
+        else:
+            y, h = ops.rmsnorm(xx, w, gw, 1e-5), xx
+        ((y * up).sum() + (h * ur).sum()).backward()
+        outs.append((y.detach(), xx.grad, gw))
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b)
+    # residual output unused: the gradient is the norm's alone
+    xx = x.clone().requires_grad_(True)
+    y, _ = ops.rmsnorm_res(xx, w, None, 1e-5)
+    (y * up).sum().backward()
+    xr = x.clone().requires_grad_(True)
+    (ops.rmsnorm(xr, w, None, 1e-5) * up).sum().backward()
+    torch.testing.assert_close(xx.grad, xr.grad)
