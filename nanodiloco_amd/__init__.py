@@ -17,8 +17,11 @@ def __getattr__(name):
     if name == "main":
         from .main import main
         return main
+    if name == "train_model":
+        from .trainer import train_model
+        return train_model
     raise AttributeError(name)
 
 
-__all__ = ["LlamaConfig", "LlamaForCausalLM", "ParamStore", "Diloco", "main", "load_config_from_file",
+__all__ = ["LlamaConfig", "LlamaForCausalLM", "ParamStore", "Diloco", "main", "train_model", "load_config_from_file",
            "default_llama_config", "default_run_config"]
