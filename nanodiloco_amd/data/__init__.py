@@ -25,20 +25,23 @@ def build_data(kind: str, *, vocab_size: int, seq_len: int, batch_size: int, see
 
 
 class _DeviceIter:
+    """Moves host batches to the device; forwards the loader's resumable cursor."""
+
     def __init__(self, loader, device):
         self.loader, self.device = loader, device
-        self._it = iter(loader)
 
     def __iter__(self):
         return self
 
     def __next__(self):
-        try:
-            b = next(self._it)
-        except StopIteration:  # epoch boundary: keep going (trainer is bounded by total_steps)
-            self._it = iter(self.loader)
-            b = next(self._it)
+        b = next(self.loader)
         return {k: v.to(self.device, non_blocking=True) for k, v in b.items()}
+
+    def state_dict(self):
+        return self.loader.state_dict()
+
+    def load_state_dict(self, d):
+        self.loader.load_state_dict(d)
 
 
 __all__ = ["SyntheticTokens", "build_data"]

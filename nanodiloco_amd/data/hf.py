@@ -8,7 +8,8 @@
 * collate = pad to the longest sequence rounded up to a multiple of 8, ``labels = input_ids``.
   Pads are masked to -100 (the reference leaves them in the loss, Q5; ``mask_pad_labels=False``
   reproduces that);
-* ``DataLoader(batch_size=per_device_batch_size, shuffle=True, drop_last=True)``.
+* ``DataLoader(batch_size=per_device_batch_size, shuffle=True, drop_last=True)`` semantics, as a
+  resumable batch iterator (:class:`HFBatches`: the cursor is checkpointed).
 
 Tokeniser: ``AutoTokenizer.from_pretrained(name)`` with ``pad_token = "</s>"`` (reference default
 ``huggyllama/llama-7b``); it must be available locally (no network on MI355X boxes).  For
@@ -55,16 +56,60 @@ def make_collate(tokenizer, seq_length: int, mask_pad_labels: bool = True):
     return collate
 
 
+class HFBatches:
+    """Resumable replacement for ``DataLoader(shard, batch_size, shuffle=True, drop_last=True,
+    collate_fn)`` (REF/nanodiloco/main.py:90-96; ``num_workers=0`` there too).
+
+    Epoch ``e`` visits the shard in the permutation drawn from ``torch.Generator().manual_seed(
+    seed + e)`` (same on every rank, like the reference's same-seed shuffle), in full batches only.
+    The cursor ``(epoch, batch)`` is the whole state, so a resumed run continues with exactly the
+    batch an uninterrupted run would have drawn.  Iterating past the last full batch of an epoch
+    moves to the next epoch (the trainer is bounded by ``total_steps``, not by epochs)."""
+
+    def __init__(self, shard, batch_size: int, collate, seed: int):
+        if len(shard) < batch_size:
+            raise ValueError(f"dataset shard has {len(shard)} rows < per-device batch {batch_size}")
+        self.shard, self.batch_size, self.collate, self.seed = shard, batch_size, collate, int(seed)
+        self.epoch, self.batch = 0, 0
+        self._perm = None
+
+    @property
+    def batches_per_epoch(self) -> int:
+        return len(self.shard) // self.batch_size
+
+    def _order(self):
+        if self._perm is None:
+            import torch
+            g = torch.Generator()
+            g.manual_seed(self.seed + self.epoch)
+            self._perm = torch.randperm(len(self.shard), generator=g).tolist()
+        return self._perm
+
+    def __iter__(self):
+        return self
+
+    def __len__(self):
+        return self.batches_per_epoch
+
+    def __next__(self):
+        if self.batch >= self.batches_per_epoch:
+            self.epoch, self.batch, self._perm = self.epoch + 1, 0, None
+        idx = self._order()[self.batch * self.batch_size:(self.batch + 1) * self.batch_size]
+        self.batch += 1
+        return self.collate([self.shard[i] for i in idx])
+
+    def state_dict(self):
+        return {"epoch": self.epoch, "batch": self.batch}
+
+    def load_state_dict(self, d):
+        self.epoch, self.batch, self._perm = int(d["epoch"]), int(d["batch"]), None
+
+
 def make_hf_loader(dataset_path: str, tokenizer_name: str, seq_length: int, per_device_batch_size: int,
-                   world_size: int, rank: int, seed: int, mask_pad_labels: bool = True):
-    import torch
+                   world_size: int, rank: int, seed: int, mask_pad_labels: bool = True) -> HFBatches:
     from datasets.distributed import split_dataset_by_node
-    from torch.utils.data import DataLoader
 
     tok = get_tokenizer(tokenizer_name)
     ds = get_tokenized_dataset(dataset_path, tok, seq_length)
     shard = split_dataset_by_node(ds, world_size=world_size, rank=rank)
-    g = torch.Generator()
-    g.manual_seed(seed)
-    return DataLoader(shard, batch_size=per_device_batch_size, collate_fn=make_collate(tok, seq_length, mask_pad_labels),
-                      drop_last=True, shuffle=True, generator=g)
+    return HFBatches(shard, per_device_batch_size, make_collate(tok, seq_length, mask_pad_labels), seed)

@@ -15,8 +15,9 @@ weights load here.  The compute graph is our own:
   loss = lm_head_ce(y, W_lm, targets)       fused chunked GEMM + CE (+ its backward)
 
 Weight gradients are written straight into ``store.grad`` by the ops' backward (and, for the
-lm head, during the forward).  ``layer_hook`` lets the trainer react as soon as a layer's
-gradients are final (used for the inner-DDP bucketed all-reduce overlapped with backward).
+lm head, during the forward).  ``layer_hook(i)`` is called from the backward as soon as every
+gradient in layer i's span is final (used for the inner-DDP bucketed all-reduce overlapped with
+backward; see ``_GradHook`` for why the hook sits on the next norm's input).
 """
 from __future__ import annotations
 
@@ -37,7 +38,13 @@ class CausalLMOutput:
 
 
 class _GradHook(torch.autograd.Function):
-    """Identity; calls ``fn(idx)`` when the gradient w.r.t. its input has been produced."""
+    """Identity; calls ``fn(idx)`` when the gradient w.r.t. its input has been produced.
+
+    Placement matters: autograd runs a node only after every consumer of its output has produced
+    its gradient, so a hook on the INPUT of the add+RMSNorm that feeds layer i fires after the whole
+    backward of layer i (GEMMs, attention, SwiGLU, both norms) -- i.e. when layer i's span of the
+    flat grad buffer is final.  (A hook on a layer's OUTPUT would fire before that layer's own
+    backward has run.)"""
 
     @staticmethod
     def forward(ctx, x, fn, idx):
@@ -204,6 +211,11 @@ class LlamaForCausalLM:
         eps = c.rms_norm_eps
         cos, sin = ops.rope_cache(T, c.head_dim, c.rope_theta, c.rope_scaling, self.device)
         h = ops.embedding(input_ids, self._m("model.embed_tokens.weight"), self._g("model.embed_tokens.weight"))
+        hook = self.layer_hook if (self.layer_hook is not None and self.training and torch.is_grad_enabled()) else None
+        if hook is not None:
+            # layer 0's last gradient (its input_layernorm weight) is written by the backward of the
+            # norm below; the hook node on the norm's INPUT runs right after that backward
+            h = _GradHook.apply(h, hook, 0)
         q = self._q8("0.qkv")
         # (y, h): the embedding output feeds both the first norm and the residual stream; rmsnorm_res
         # fuses the two gradient contributions inside the norm's backward kernel
@@ -218,8 +230,10 @@ class LlamaForCausalLM:
                 m, h = checkpoint(self._layer, i, h, y, cos, sin, B, T, nxt, None, use_reentrant=False)
             else:
                 m, h = self._layer(i, h, y, cos, sin, B, T, nxt, y8)
-            if self.layer_hook is not None and torch.is_grad_enabled():
-                h = _GradHook.apply(h, self.layer_hook, i)
+            if hook is not None and i + 1 < L:
+                # layer i+1's gradients are final once the backward of the add+norm that produces its
+                # input (and owns its input_layernorm weight) has run: hook that norm's input
+                m = _GradHook.apply(m, hook, i + 1)
             q = self._q8(f"{i + 1}.qkv") if i + 1 < L else None
             y, h = ops.add_rmsnorm(h, m, self._m(nxt), self._g(nxt), eps, cdt, q8=q,
                                    q8_bwd=self._q8(f"{i}.down", grad=True))

@@ -133,6 +133,8 @@ class Diloco:
         self.local_step += 1
         if self._pending is not None:  # overlapped outer step from the previous boundary
             self._finish_outer()
+        if self.debug_checks and self.env.inner_dp > 1:
+            self.check_inner_replicas()
 
     # ------------------------------------------------------------------ outer step
     def outer_step(self):
@@ -205,22 +207,50 @@ class Diloco:
             self._finish_outer()
 
     # ------------------------------------------------------------------ debug
+    @staticmethod
+    def _checksum_spread(x: torch.Tensor, group) -> torch.Tensor:
+        """MAX-MIN over ``group`` of two order-sensitive fp64 checksums of ``x``."""
+        import torch.distributed as dist
+        xd = x.double()
+        w = torch.arange(1, x.numel() + 1, device=x.device, dtype=torch.float64).remainder(7)
+        v = torch.stack([xd.sum(), (xd * w).sum()])
+        mx, mn = v.clone(), v.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
+        return (mx - mn).abs()
+
     @torch.no_grad()
     def check_replicas(self, tol: float = 0.0):
-        """Assert all replicas hold identical outer weights theta_sync: checksum
-        all-reduce MAX-MIN.  (In the overlapped mode the local weights legitimately differ by each
-        worker's in-flight inner progress, so the synced snapshot is what must agree.)"""
+        """Replica-consistency assertions, run after every outer step with
+        ``debug_checks``:
+
+        * theta_sync is identical on every rank of the job;
+        * the GPUs of one DiLoCo worker (inner DDP) hold identical master weights;
+        * without the overlapped outer step, the master weights equal theta_sync everywhere.
+        (In the overlapped mode the local weights legitimately differ across workers by each
+        worker's in-flight inner progress.)"""
         if not self.env.is_distributed:
             return
-        import torch.distributed as dist
-        m = self.sync.to(self.store.device)
-        v = torch.stack([m.double().sum(), (m.double() * torch.arange(1, m.numel() + 1, device=m.device,
-                                                                      dtype=torch.float64).remainder(7)).sum()])
-        mx, mn = v.clone(), v.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
-        if (mx - mn).abs().max().item() > tol:
-            raise RuntimeError(f"DiLoCo replicas diverged: checksum spread {(mx - mn).tolist()}")
+        spread = self._checksum_spread(self.sync.to(self.store.device), None)
+        if spread.max().item() > tol:
+            raise RuntimeError(f"DiLoCo replicas diverged: theta_sync checksum spread {spread.tolist()}")
+        self.check_inner_replicas(tol)
+        if not self.overlap and self._pending is None:
+            spread = self._checksum_spread(self.store.master, None)
+            if spread.max().item() > tol:
+                raise RuntimeError(f"DiLoCo replicas diverged: master checksum spread {spread.tolist()}")
+
+    @torch.no_grad()
+    def check_inner_replicas(self, tol: float = 0.0):
+        """The K GPUs of one DiLoCo worker apply the same all-reduced gradient every inner step, so
+        their master weights must stay bit-identical (run after every inner step with
+        ``debug_checks`` when ``inner_dp > 1``)."""
+        if self.env.inner_dp <= 1:
+            return
+        spread = self._checksum_spread(self.store.master, self.env.inner_group)
+        if spread.max().item() > tol:
+            raise RuntimeError(f"inner-DDP replicas diverged inside worker {self.env.worker}: "
+                               f"master checksum spread {spread.tolist()}")
 
     # ------------------------------------------------------------------ checkpoint state
     def state_dict(self):
@@ -235,9 +265,11 @@ class Diloco:
         }
 
     def load_state_dict(self, d):
+        """Restore the outer state (``inner`` is optional: the checkpoint keeps AdamW state per rank)."""
         self.sync.copy_(d["sync"])
         self.outer_optimizer.load_state_dict(d["outer"])
-        self.inner_optimizer.load_state_dict(d["inner"])
+        if "inner" in d:
+            self.inner_optimizer.load_state_dict(d["inner"])
         self.scheduler.load_state_dict(d["scheduler"])
         self.local_step = int(d["local_step"])
         self.outer_step_count = int(d["outer_step_count"])

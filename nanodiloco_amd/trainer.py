@@ -150,11 +150,17 @@ class Trainer:
             from .utils.checkpoint import load_checkpoint
             st = load_checkpoint(a.resume, self.model, self.diloco, e)
             self.start_step = int(st["step"])
-            if st.get("data_state") and hasattr(self.data, "load_state_dict"):
-                try:
-                    self.data.load_state_dict(st["data_state"])
-                except Exception:
-                    pass
+            ds = st.get("data_state")
+            if ds:
+                # a data stream that cannot be restored must fail the resume loudly: silently
+                # restarting it would re-train on the same tokens
+                if not hasattr(self.data, "load_state_dict"):
+                    raise RuntimeError(f"checkpoint has data state but data source {self.data_kind!r} "
+                                       f"cannot restore it")
+                self.data.load_state_dict(ds)
+            elif hasattr(self.data, "load_state_dict"):
+                raise RuntimeError(f"checkpoint {a.resume} has no data state for rank {e.rank}; "
+                                   f"resuming would restart the data stream")
         self.graphed = None
         hg = str(a.hip_graph).lower()
         if hg == "auto":

@@ -37,6 +37,11 @@ def _load_st(path: str) -> Dict[str, torch.Tensor]:
 def save_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, step: int, data_state: Optional[Dict[str, Any]] = None,
                     extra: Optional[Dict[str, Any]] = None):
     diloco.finalize()
+    if env.inner_dp > 1:
+        # two-level mode: each GPU of a worker updates only its shard of the outer momentum
+        # (parallel/diloco.py, sharded outer step); gather the worker's full buffer before rank 0
+        # writes it, so a resumed run restores every shard (not just shard 0)
+        diloco.inner_comm.all_gather_flat(diloco.outer_optimizer.momentum_buffer, diloco.shards, env.inner_rank)
     os.makedirs(ckpt_dir, exist_ok=True)
     store = model.store
     r = env.rank
@@ -75,12 +80,10 @@ def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv) -> Dict[str, Any
     sd = _load_st(os.path.join(ckpt_dir, "model.safetensors"))
     model.load_state_dict(sd)
     ds = _load_st(os.path.join(ckpt_dir, "diloco_state.safetensors"))
-    diloco.sync.copy_(ds["theta_sync"])
-    diloco.outer_optimizer.momentum_buffer.copy_(ds["outer_momentum"])
-    diloco.outer_optimizer.step_count = int(state["outer_opt_step"])
-    diloco.scheduler.load_state_dict(state["scheduler"])
-    diloco.local_step = int(state["local_step"])
-    diloco.outer_step_count = int(state["outer_step_count"])
+    diloco.load_state_dict({"sync": ds["theta_sync"],
+                            "outer": {"momentum_buffer": ds["outer_momentum"], "step": state["outer_opt_step"]},
+                            "scheduler": state["scheduler"], "local_step": state["local_step"],
+                            "outer_step_count": state["outer_step_count"]})
     rfile = os.path.join(ckpt_dir, f"rank{env.rank}.safetensors")
     data_state: Dict[str, Any] = {}
     if os.path.exists(rfile):

@@ -6,6 +6,7 @@ import subprocess
 import sys
 
 import pytest
+import torch
 
 from ._mp import free_port
 
@@ -53,19 +54,37 @@ def test_two_level_and_overlap(tmp_path):
                          "--log-every", "4"], tmp_path)
 
 
+def _tensors(path):
+    from safetensors.torch import load_file
+    return load_file(str(path))
+
+
 @pytest.mark.slow
-def test_resume_matches_uninterrupted(tmp_path):
+@pytest.mark.parametrize("nproc,inner_dp", [(2, 1), (4, 2)])
+def test_resume_matches_uninterrupted(tmp_path, nproc, inner_dp):
+    """Stop after 2 outer steps, resume, finish: bit-identical to the uninterrupted run -- weights,
+    theta_sync and (two-level mode) every shard of the outer momentum."""
     a, b = tmp_path / "a", tmp_path / "b"
     la, lb = tmp_path / "a.jsonl", tmp_path / "b.jsonl"
-    common = BASE + ["--inner-steps", "2", "--data", "synthetic"]
-    _torchrun(2, common + ["--total-steps", "6", "--checkpoint-dir", str(a), "--log-file", str(la)], tmp_path)
+    common = BASE + ["--inner-steps", "2", "--data", "synthetic", "--inner-dp", str(inner_dp)]
+    _torchrun(nproc, common + ["--total-steps", "6", "--checkpoint-dir", str(a), "--log-file", str(la)], tmp_path)
     # interrupted run: 4 steps + checkpoint every outer step, then resume to 6
-    _torchrun(2, common + ["--total-steps", "6", "--stop-at-step", "4", "--checkpoint-dir", str(b),
-                         "--checkpoint-every", "1"], tmp_path)
-    _torchrun(2, common + ["--total-steps", "6", "--resume", str(b), "--log-file", str(lb)], tmp_path)
+    _torchrun(nproc, common + ["--total-steps", "6", "--stop-at-step", "4", "--checkpoint-dir", str(b),
+                               "--checkpoint-every", "1"], tmp_path)
+    _torchrun(nproc, common + ["--total-steps", "6", "--resume", str(b), "--log-file", str(lb),
+                               "--checkpoint-dir", str(b)], tmp_path)
     ra, rb = _log(la), _log(lb)
     assert [x["step"] for x in rb] == [5, 6]
-    assert abs(ra[-1]["loss"] - rb[-1]["loss"]) < 1e-5
+    assert ra[-1]["loss"] == rb[-1]["loss"]
+    for f in ("model.safetensors", "diloco_state.safetensors"):
+        ta, tb = _tensors(a / f), _tensors(b / f)
+        assert ta.keys() == tb.keys()
+        for k in ta:
+            assert torch.equal(ta[k], tb[k]), (f, k)
+    mom = _tensors(a / "diloco_state.safetensors")["outer_momentum"]
+    if inner_dp > 1:  # every shard carries momentum, not only shard 0
+        n = mom.numel() // inner_dp
+        assert all(mom[i * n:(i + 1) * n].abs().sum() > 0 for i in range(inner_dp))
 
 
 def _bench_json(stdout: str) -> dict:

@@ -41,7 +41,9 @@ def test_hf_loader_pads_masks_and_shards(tmp_path):
     for rank in range(2):
         dl = make_hf_loader(ds, tok, seq_length=16, per_device_batch_size=4, world_size=2, rank=rank, seed=0)
         n = 0
-        for b in dl:
+        assert len(dl) == 4
+        for _ in range(len(dl)):
+            b = next(dl)
             ids, lab, am = b["input_ids"], b["labels"], b["attention_mask"]
             assert ids.shape[1] % 8 == 0 and ids.shape[0] == 4
             assert torch.equal(lab[am == 1], ids[am == 1])
@@ -61,3 +63,19 @@ def test_trainer_hf_path_runs(tmp_path):
                             inner_steps=2, dataset_path=ds, tokenizer=tok, llama_config_file=str(cfg), wandb="off",
                             device="cpu", data="hf")).train()
     assert out["steps"] == 4 and out["outer_steps"] == 2
+
+
+def test_hf_loader_resumes_from_cursor(tmp_path):
+    from nanodiloco_amd.data.hf import make_hf_loader
+    tok, ds = _tokenizer(tmp_path), _dataset(tmp_path)
+    mk = lambda: make_hf_loader(ds, tok, seq_length=16, per_device_batch_size=4, world_size=2, rank=1, seed=3)
+    a = mk()
+    for _ in range(6):  # crosses the epoch boundary (4 batches per epoch)
+        next(a)
+    st = a.state_dict()
+    assert st == {"epoch": 1, "batch": 2}
+    b = mk()
+    b.load_state_dict(st)
+    for _ in range(5):
+        x, y = next(a), next(b)
+        assert torch.equal(x["input_ids"], y["input_ids"]) and torch.equal(x["labels"], y["labels"])
