@@ -172,6 +172,11 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    outer_ms = dl.comm_ms()  # device time of the last outer step (HIP events; after the timed window)
+    if env.is_distributed:
+        t = torch.tensor([outer_ms], dtype=torch.float64, device=env.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        outer_ms = float(t.item())
     tokens = a.batch_size * a.seq_len * a.steps * env.world_size
     tps = tokens / elapsed
     final_loss = float((loss / accum).item()) if loss is not None else float("nan")
@@ -212,6 +217,13 @@ def main():
             "bytes_per_outer_step": dl.bytes_per_outer_step if env.num_workers > 1 else model.store.numel * (
                 2 if comm_dtype == torch.bfloat16 else 4),
             "outer_steps_in_window": n_outer,
+            # outer-step cost as seen by the compute stream (HIP events: pseudo-gradient + bucketed
+            # RCCL all-reduce + fused Nesterov), host wall time per outer step, and calls per outer step
+            "outer_step_ms": round(outer_ms, 3),
+            "outer_step_wall_ms": round(1000.0 * dl.avg_sync_time, 3),
+            "allreduce_calls_per_outer_step": dl.buckets_per_outer_step,
+            "comm_backend": env.backend,
+            "comm_dtype": a.comm_dtype,
             "model_tflops_per_gpu": round(mfu_flops / 1e12, 2),
             "final_loss": round(final_loss, 4),
             "tuned_gemm": enable_tuned_gemms(env.device) if env.device.type == "cuda" and not a.no_tuned_gemm else False,

@@ -111,12 +111,22 @@ class Diloco:
         return (b - a) * torch.tensor([], dtype=self.comm_dtype).element_size() if self.env.num_workers > 1 else 0
 
     def comm_ms(self) -> float:
-        """Device time of the last outer step's collectives (HIP events; syncs on them)."""
+        """Device time of the last outer step (HIP events on the compute stream, from the pseudo-
+        gradient kernel to the last outer-Nesterov / all-gather: i.e. everything the outer step
+        costs the compute stream, collectives included; syncs on the end event)."""
         if not self._comm_events:
             return 0.0
         s, e = self._comm_events[-1]
         e.synchronize()
         return s.elapsed_time(e)
+
+    @property
+    def buckets_per_outer_step(self) -> int:
+        """Number of all-reduce calls one outer step issues (the reference issues one per tensor)."""
+        if self.env.num_workers <= 1:
+            return 0
+        a, b = self.my_shard
+        return len(plan_buckets(0, b - a, self.delta.element_size(), self.outer_comm.bucket_bytes))
 
     def current_lr(self) -> float:
         return self.scheduler.lr()
@@ -148,7 +158,12 @@ class Diloco:
         a, b = self.my_shard
         ops.pseudograd(sync[a:b], master[a:b], self.delta)
         if self.overlap:
-            self.drift_base.copy_(self.delta)
+            # fp32 drift base: with bf16 transport, re-applying the local progress from the rounded
+            # delta would carry its bf16 rounding error into the weights every outer step
+            if self.delta.dtype == torch.float32:
+                self.drift_base.copy_(self.delta)
+            else:
+                ops.pseudograd(sync[a:b], master[a:b], self.drift_base)
         pend = self.outer_comm.all_reduce_async(self.delta)
         self._pending = (pend, sync, ev0, t0)
         self.outer_step_count += 1

@@ -156,3 +156,27 @@ def test_skip_nonfinite_step():
     g[3] = 0.0
     adamw_step(master, g, m, v, None, 1, 1e-3, skip_nonfinite=True, skipped=skipped)
     assert not torch.equal(master, before) and int(skipped.item()) == 1
+
+
+def _overlap_bf16_exact_drift(rank, world):
+    """Overlapped + bf16 transport: the re-applied local progress is exact (fp32 drift base); only
+    the averaged pseudo-gradient itself carries bf16 rounding."""
+    env, m, dl = _mk(rank, overlap=True, comm=torch.bfloat16, seed=5)
+    st = m.store
+    base = st.master.clone()
+    drift = torch.full_like(base, -(rank + 1.0))
+    drift[: st.num_params] += 1e-3 * torch.arange(st.num_params).remainder(13)  # not bf16-representable
+    st.master.add_(drift)
+    dl.outer_step()
+    local_after = st.master.clone()
+    st.master.add_(0.25)
+    dl.finalize()
+    # master - sync_new must equal the local progress since the boundary EXACTLY: (base+drift+0.25) - (base+drift)
+    progress = (st.master - dl.sync)[: st.num_params]
+    exact = ((local_after + 0.25) - local_after)[: st.num_params]
+    assert torch.allclose(progress, exact, atol=1e-6), (progress - exact).abs().max()
+    return True
+
+
+def test_overlapped_bf16_transport_keeps_fp32_drift():
+    assert all(run_ranks(_overlap_bf16_exact_drift, 2))
