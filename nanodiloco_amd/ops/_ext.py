@@ -159,8 +159,11 @@ def _declare(L: ctypes.CDLL):
         # fp8 quantisation
         "nd_fp8_cast": [P, I, L64, P, P, I, P, I, P],
         "nd_fp8_cast_t": [P, I, I, I, L64, P, P, P, I, P, I, P],
-        # forward-projection GEMM (C = A B^T)
-        "nd_gemm_nt": [P, P, P, I, I, I, L64, L64, L64, P, P],
+        # projection GEMMs (C = A B^T) and their fused epilogues
+        "nd_gemm_nt": [P, P, P, I, I, I, L64, L64, L64, P],
+        "nd_gemm_nt_rope": [P, P, P, I, I, I, L64, L64, L64, P, P, I, I, I, P],
+        "nd_gemm_nt_swiglu": [P, P, P, P, I, I, I, L64, L64, L64, L64, P],
+        "nd_gemm_nt_dswiglu": [P, P, P, P, I, I, I, L64, L64, L64, L64, P],
         # weight-gradient GEMM
         "nd_wgrad_splits": [I, I, I],
         "nd_wgrad": [P, P, P, P, I, I, I, L64, L64, L64, P],

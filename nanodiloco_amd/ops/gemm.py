@@ -1,9 +1,19 @@
-"""Weight-gradient GEMM on the HIP path (``nd_wgrad``): ``gW[M, N] (fp32) += dY[K, M]^T @ X[K, N]``.
+"""Own MFMA GEMMs (csrc/gemm.hip, csrc/gemm_wgrad.hip).
 
-hipBLASLt runs this token-reduction layout at 330-900 TF/s on the Llama-150M shapes (profiles/),
-because K (tokens) is the strided axis of both operands; the custom kernel stages both operands
-through LDS as they lie in memory and forms MFMA fragments with transposing LDS reads, with a
-deterministic split-K for the small outputs.  Plain fwd / dgrad GEMMs stay on hipBLASLt.
+* ``gemm_nt``        C[M, N] = A[M, K] . B[N, K]^T -- every projection forward and (with the W^T copies
+                     of ops/linear.py) every input-gradient GEMM, the lm-head logits and dgrad.
+* ``gemm_nt_rope``   the q|k|v projection with RoPE applied to q and k in the epilogue.
+* ``gemm_nt_swiglu`` the gate|up projection writing gu AND act = silu(gate) * up.
+* ``gemm_nt_dswiglu``the down projection's input gradient fused with the SwiGLU backward: writes
+                     d(gate|up) straight from the accumulator (d(act) never stored).
+* ``wgrad``          ``gW[M, N] (fp32) += dY[K, M]^T @ X[K, N]`` -- the token-reduction layout hipBLASLt
+                     runs at 330-900 TF/s on the Llama-150M shapes: both operands are staged through LDS
+                     as they lie in memory and fragments formed with transposing LDS reads, with a
+                     deterministic split-K for the small outputs.
+
+``set_gemm_backend("blas")`` routes the NT GEMMs back to hipBLASLt (``torch.mm``) for A/B runs; the
+default on a GPU is our kernels.  Shapes outside ``nt_supported`` (K % 64, N % 4, alignment) use
+hipBLASLt.
 """
 from __future__ import annotations
 
@@ -12,6 +22,76 @@ import torch
 from . import _ext
 
 _WS = {}
+_GEMM = {"backend": "hip"}
+
+
+def set_gemm_backend(name: str) -> None:
+    """'hip': own MFMA kernels for the projection GEMMs (default); 'blas': hipBLASLt (A/B)."""
+    if name not in ("hip", "blas"):
+        raise ValueError(name)
+    _GEMM["backend"] = name
+
+
+def gemm_backend() -> str:
+    return _GEMM["backend"]
+
+
+def _aligned(t: torch.Tensor) -> bool:
+    return t.data_ptr() % 16 == 0 and t.stride(-1) == 1 and t.stride(0) % 8 == 0
+
+
+def nt_supported(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Can ``gemm_nt(a, b)`` (C = a . b^T) run on the own kernel?"""
+    return (_GEMM["backend"] == "hip" and a.is_cuda and _ext.get_backend() != "torch"
+            and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
+            and a.shape[1] == b.shape[1] and a.shape[1] % 64 == 0 and b.shape[0] % 4 == 0
+            and _aligned(a) and _aligned(b))
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """out[M, N] = a[M, K] . b[N, K]^T (bf16, fp32 accumulate)."""
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_nt(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0), b.stride(0),
+                                     out.stride(0), _ext.stream_ptr(a.device)), "nd_gemm_nt")
+    return out
+
+
+def gemm_nt_rope(a, b, cos, sin, T: int, hd: int, rope_cols: int, out=None) -> torch.Tensor:
+    """q|k|v projection with RoPE on the first ``rope_cols`` columns (tokens are rows, t = row % T)."""
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_nt_rope(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0), b.stride(0),
+                                          out.stride(0), _ext.ptr(cos), _ext.ptr(sin), T, hd, rope_cols,
+                                          _ext.stream_ptr(a.device)), "nd_gemm_nt_rope")
+    return out
+
+
+def gemm_nt_swiglu(a, w_gu, gu_out=None, act_out=None):
+    """(gu, act): gu = a . w_gu^T ([M, 2F]), act = silu(gu[:, :F]) * gu[:, F:] ([M, F])."""
+    M, K = a.shape
+    F = w_gu.shape[0] // 2
+    gu = gu_out if gu_out is not None else torch.empty(M, 2 * F, dtype=a.dtype, device=a.device)
+    act = act_out if act_out is not None else torch.empty(M, F, dtype=a.dtype, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_nt_swiglu(_ext.ptr(a), _ext.ptr(w_gu), _ext.ptr(gu), _ext.ptr(act), M, F, K,
+                                            a.stride(0), w_gu.stride(0), gu.stride(0), act.stride(0),
+                                            _ext.stream_ptr(a.device)), "nd_gemm_nt_swiglu")
+    return gu, act
+
+
+def gemm_nt_dswiglu(dy, w_down_t, gu, dgu_out=None):
+    """d(gate|up) [M, 2F] of act = silu(gate) * up, where d(act) = dy . w_down_t^T (never stored)."""
+    M, K = dy.shape
+    F = w_down_t.shape[0]
+    dgu = dgu_out if dgu_out is not None else torch.empty_like(gu)
+    _ext.check(_ext.lib().nd_gemm_nt_dswiglu(_ext.ptr(dy), _ext.ptr(w_down_t), _ext.ptr(gu), _ext.ptr(dgu), M, F, K,
+                                             dy.stride(0), w_down_t.stride(0), gu.stride(0), dgu.stride(0),
+                                             _ext.stream_ptr(dy.device)), "nd_gemm_nt_dswiglu")
+    return dgu
 
 
 def _workspace(device, numel):

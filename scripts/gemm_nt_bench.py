@@ -1,24 +1,23 @@
 #!/usr/bin/env python3
-"""nd_gemm_nt (C = A B^T, forward-projection layout) vs hipBLASLt torch.mm on the Llama shapes:
-correctness vs fp32, then interleaved timing (min over rounds)."""
+"""Own projection GEMMs (csrc/gemm.hip) vs hipBLASLt (torch.mm) on the Llama-150M / 1B shapes, in one
+process, interleaved rounds, random operands; the fused epilogues are compared against the
+library GEMM + the separate kernel they replace.
+
+    python scripts/gemm_nt_bench.py [--tokens 65536] [--model 150m|1b] [--rounds 5]
+"""
+import argparse
 import os
 import sys
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nanodiloco_amd import ops  # noqa: E402
 from nanodiloco_amd.ops import _ext  # noqa: E402
+from nanodiloco_amd.ops import gemm as G  # noqa: E402
 
 
-def gemm_nt(a, b, c, dbg=None):
-    M, K = a.shape
-    N = b.shape[0]
-    _ext.check(_ext.lib().nd_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, a.stride(0), b.stride(0),
-                                     c.stride(0), dbg.data_ptr() if dbg is not None else 0, _ext.stream_ptr()),
-               "nd_gemm_nt")
-
-
-def timed(fn, iters=20):
+def timed(fn, iters=10):
     fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -27,35 +26,83 @@ def timed(fn, iters=20):
         fn()
     e.record()
     e.synchronize()
-    return s.elapsed_time(e) / iters * 1e3
+    return s.elapsed_time(e) / iters * 1e3  # us
 
 
 def main():
-    T = int(os.environ.get("TOKENS", 32768))
-    shapes = {"qkv": (3072, 1024), "o": (1024, 1024), "gate_up": (5376, 1024), "down": (1024, 2688),
-              "lm_head": (32000, 1024), "odd": (1000, 320)}
-    for name, (N, K) in shapes.items():
-        M = T if name not in ("lm_head", "odd") else (16384 if name == "lm_head" else 777)
-        a = torch.randn(M, K, device="cuda").bfloat16()
-        b = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
-        c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        gemm_nt(a, b, c)
-        ref = a.float() @ b.float().t()
-        err = ((c.float() - ref).norm() / ref.norm()).item()
-        fl = 2.0 * M * N * K
-        t_n, t_b = [], []
-        for _ in range(3):
-            t_n.append(timed(lambda: gemm_nt(a, b, c)))
-            t_b.append(timed(lambda: torch.mm(a, b.t())))
-        tiles = ((M + 255) // 256) * ((N + 255) // 256)
-        dbg = torch.zeros(tiles * 8 * 4, dtype=torch.int64, device="cuda")
-        gemm_nt(a, b, c, dbg)
-        torch.cuda.synchronize()
-        d = dbg.view(-1, 4).double()
-        stamp = (f"  [stamps: boundary wait {d[:, 0].sum() / d[:, 2].sum():.0%}, lds wait "
-                 f"{d[:, 1].sum() / d[:, 2].sum():.0%} of wave time; clock {d[:, 2].sum() / d[:, 3].sum() * 0.1:.2f} GHz]")
-        print(f"{name:8s} M={M} N={N} K={K}  err={err:.1e}  ours {min(t_n):7.1f} us {fl / min(t_n) / 1e6:6.0f} TF/s | "
-              f"hipBLASLt {min(t_b):7.1f} us {fl / min(t_b) / 1e6:6.0f} TF/s" + stamp, flush=True)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=int, default=65536)
+    ap.add_argument("--model", default="150m")
+    ap.add_argument("--rounds", type=int, default=5)
+    a = ap.parse_args()
+    ops.set_backend("hip")
+    M = a.tokens
+    d, F, nh, nkv, hd, V = (1024, 2688, 16, 16, 64, 32000) if a.model == "150m" else (2048, 5632, 32, 4, 64, 32000)
+    qkv_n = (nh + 2 * nkv) * hd
+    T = 1024
+    cos, sin = ops.rope_cache(T, hd, 10000.0, None, "cuda")
+    r = lambda *s: (torch.rand(*s, device="cuda") * 2 - 1).bfloat16()  # noqa: E731
+    cases = []
+
+    def plain(name, m, n, k):
+        x, w = r(m, k), r(n, k) * 0.05
+        out = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+        cases.append((name, 2.0 * m * n * k, lambda: G.gemm_nt(x, w, out), lambda: torch.mm(x, w.t(), out=out)))
+
+    plain("qkv fwd", M, qkv_n, d)
+    plain("o fwd", M, d, nh * hd)
+    plain("gu fwd", M, 2 * F, d)
+    plain("down fwd", M, d, F)
+    plain("qkv dgrad", M, d, qkv_n)
+    plain("o dgrad", M, nh * hd, d)
+    plain("gu dgrad", M, d, 2 * F)
+    plain("down dgrad", M, F, d)
+    plain("lm logits", 16384, V, d)
+    plain("lm dgrad", 16384, d, V)
+    # fused epilogues vs library GEMM + the separate kernel
+    x, wq = r(M, d), r(qkv_n, d) * 0.05
+    qo = torch.empty(M, qkv_n, device="cuda", dtype=torch.bfloat16)
+
+    def rope_lib():
+        torch.mm(x, wq.t(), out=qo)
+        _ext.check(_ext.lib().nd_rope_inplace(qo.data_ptr(), 1, cos.data_ptr(), sin.data_ptr(), M, T, nh, nkv, hd,
+                                              qkv_n, 0, _ext.stream_ptr()), "rope")
+
+    cases.append(("qkv+rope", 2.0 * M * qkv_n * d, lambda: G.gemm_nt_rope(x, wq, cos, sin, T, hd, (nh + nkv) * hd, qo),
+                  rope_lib))
+    wg = r(2 * F, d) * 0.05
+    gu = torch.empty(M, 2 * F, device="cuda", dtype=torch.bfloat16)
+    act = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+
+    def swiglu_lib():
+        torch.mm(x, wg.t(), out=gu)
+        _ext.check(_ext.lib().nd_swiglu_fwd(gu.data_ptr(), act.data_ptr(), 1, M, F, _ext.stream_ptr()), "swiglu")
+
+    cases.append(("gu+swiglu", 2.0 * M * 2 * F * d, lambda: G.gemm_nt_swiglu(x, wg, gu, act), swiglu_lib))
+    dy, wdt = r(M, d), r(F, d) * 0.05
+    gu_in = r(M, 2 * F)
+    dgu = torch.empty(M, 2 * F, device="cuda", dtype=torch.bfloat16)
+    dact = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+
+    def dswiglu_lib():
+        torch.mm(dy, wdt.t(), out=dact)
+        _ext.check(_ext.lib().nd_swiglu_bwd(dact.data_ptr(), gu_in.data_ptr(), dgu.data_ptr(), 1, M, F,
+                                            _ext.stream_ptr()), "swiglu_bwd")
+
+    cases.append(("down dgrad+dswiglu", 2.0 * M * F * d, lambda: G.gemm_nt_dswiglu(dy, wdt, gu_in, dgu), dswiglu_lib))
+
+    tot_o = tot_b = 0.0
+    for name, fl, ours, lib in cases:
+        to, tb = [], []
+        for _ in range(a.rounds):
+            to.append(timed(ours))
+            tb.append(timed(lib))
+        o, b = sorted(to)[len(to) // 2], sorted(tb)[len(tb) // 2]
+        tot_o += o
+        tot_b += b
+        print(f"{name:20s} ours {o:8.1f} us {fl / o / 1e6:6.0f} TF/s | hipBLASLt(+kernel) {b:8.1f} us "
+              f"{fl / b / 1e6:6.0f} TF/s | ours/lib {b / o:5.3f}x", flush=True)
+    print(f"{'TOTAL':20s} ours {tot_o:8.1f} us | lib {tot_b:8.1f} us | {tot_b / tot_o:5.3f}x", flush=True)
 
 
 if __name__ == "__main__":

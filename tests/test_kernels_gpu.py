@@ -324,18 +324,6 @@ def test_adamw_skip_nonfinite_on_device():
     assert torch.equal(master, before) and int(skipped.item()) == 1
 
 
-# ----------------------------------------------------------------------------------- NT GEMM (experimental)
-@pytest.mark.parametrize("M,N,K", [(1024, 768, 512), (777, 1000, 320), (4096, 256, 1024)])
-def test_gemm_nt(M, N, K):
-    from nanodiloco_amd.ops import _ext
-    a = torch.randn(M, K, device=DEV).bfloat16()
-    b = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
-    c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    _ext.check(_ext.lib().nd_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, K, K, N, 0,
-                                     _ext.stream_ptr()), "nd_gemm_nt")
-    assert rel(c, a.float() @ b.float().t()) < 5e-3
-
-
 # ----------------------------------------------------------------------------------- transpose
 @pytest.mark.parametrize("rows,cols", [(3072, 1024), (1024, 2688), (100, 72), (32000, 1024)])
 def test_transpose_bf16(rows, cols):
