@@ -40,6 +40,16 @@ from .dist import DistEnv
 
 
 class Diloco:
+    """Flagship DiLoCo on the flat-store Llama.  Any other ``nn.Module`` (with plain torch optimizers)
+    is dispatched to :class:`~nanodiloco_amd.parallel.module_diloco.ModuleDiloco`, which has the
+    reference's generic ``model.parameters()`` / ``param_groups`` contract."""
+
+    def __new__(cls, model, *args, **kwargs):
+        if not isinstance(model, LlamaForCausalLM):
+            from .module_diloco import ModuleDiloco
+            return ModuleDiloco(model, *args, **kwargs)
+        return super().__new__(cls)
+
     def __init__(self, model: LlamaForCausalLM, inner_optimizer: FlatAdamW, outer_optimizer: FlatOuterNesterov,
                  warmup_steps: int, total_steps: int, inner_steps: int = 100, outer_steps: Optional[int] = None,
                  env: Optional[DistEnv] = None, comm_dtype: torch.dtype = torch.float32, bucket_mb: float = 128.0,
