@@ -13,6 +13,7 @@ import concurrent.futures as cf
 import glob
 import hashlib
 import os
+import shlex
 import shutil
 import subprocess
 import sys
@@ -71,6 +72,7 @@ def build(force: bool = False, jobs: int = 0, save_temps: bool = False, verbose:
     headers = glob.glob(os.path.join(HERE, "*.h"))
     sources = sorted(glob.glob(os.path.join(HERE, "*.hip")))
     flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-I", HERE]
+    flags += shlex.split(os.environ.get("ND_EXTRA_HIPCC_FLAGS", ""))  # A/B or ablation builds only
     if save_temps:
         flags += ["-save-temps"]
     todo = []

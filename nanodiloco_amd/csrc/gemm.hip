@@ -37,6 +37,7 @@
 // XCD-aware workgroup order: consecutive output tiles (sharing an A row-panel) run on one XCD's L2.
 #include "common.h"
 #include <cstdlib>
+#include <type_traits>
 
 using namespace nd;
 
@@ -75,12 +76,64 @@ __device__ __forceinline__ void glds(const void* sbase, uint32_t voff, uint32_t 
                : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
 }
 
+// the same piece through a buffer descriptor (buffer_load_dwordx4 ... offen lds): 32-bit per-lane
+// offsets against a wave-uniform base in four SGPRs
+__device__ __forceinline__ void glds_buf(__amdgpu_buffer_rsrc_t rsrc, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_n(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+// bf16-pack the 4-column quads of two adjacent 16-column blocks (x = block b, y = block b + 1) and
+// v_permlane16_swap them so lane rows 0 / 2 hold 8 consecutive columns of block b and rows 1 / 3
+// those of block b + 1 (rows 0 / 1: columns 0-7, rows 2 / 3: columns 8-15)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 pair16(const f32x4& x, const f32x4& y) {
+  const auto s0 = __builtin_amdgcn_permlane16_swap(pack2(x[0], x[1]), pack2(y[0], y[1]), false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(pack2(x[2], x[3]), pack2(y[2], y[3]), false, false);
+  u32x4 d = u32x4{s0[0], s1[0], s0[1], s1[1]};
+  asm volatile("s_nop 1" : "+v"(d));  // permlane result -> store data: keep two wait states
+  return d;
+}
+__device__ __forceinline__ float round_bf(float x) { return lo_bf(pack2(x, 0.f)); }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7FFFFFFF, 0x00020000);
+}
+
 // element offset of (row, k) in a [128][64] K-major half-tile (chunk swizzle (row >> 1) & 7)
 __device__ __forceinline__ int koff(int row, int k) { return row * 64 + ((((k >> 3) ^ ((row >> 1) & 7))) << 3) + (k & 7); }
 
 __device__ __forceinline__ bf16x8 frag(const bf16_t* half, int row, int kc) {
   return *reinterpret_cast<const bf16x8*>(&half[koff(row, kc)]);
 }
+
+// chunk swizzle of the 4-wave kernel: SWZ 0 = (row >> 1) & 7 (conflict-free ds_read_b128, but the
+// LDS-DMA source order inside a 64-B half is permuted); SWZ 1 = swap the two 64-B halves of odd
+// row pairs only (each lane quad reads 64 ascending contiguous bytes; 2-way read conflicts)
+template <int SWZ>
+__device__ __forceinline__ int swz(int row) { return SWZ == 0 ? ((row >> 1) & 7) : (((row >> 1) & 1) << 2); }
+// SWZ 2: padded block layout.  A half-tile is 16 LDS blocks of 1056 B (8 rows x 128 B + 32 B pad);
+// block b holds rows b, b + 16, ..., b + 112 unswizzled, so every LDS-DMA lane octet reads one whole
+// 128-B row in ascending order (one cache access per line), and a ds_read_b128 lane group (16 rows
+// 16 apart in block index) lands on 16 distinct 16-B bank slots thanks to the 32-B pad.
+constexpr int BLOCK_P = 1056;                 // bytes per padded block
+constexpr int HALF_P = 16 * BLOCK_P / 2;      // elements per padded half-tile
+template <int SWZ>
+__device__ __forceinline__ bf16x8 fragz(const bf16_t* half, int row, int kc) {
+  if constexpr (SWZ == 2)
+    return *reinterpret_cast<const bf16x8*>(&half[(row & 15) * (BLOCK_P / 2) + (row >> 4) * 64 + kc]);
+  return *reinterpret_cast<const bf16x8*>(&half[row * 64 + (((kc >> 3) ^ swz<SWZ>(row)) << 3) + (kc & 7)]);
+}
+
+// the same MFMA with the accumulator pinned to AGPRs (tied "+a" operand): hipcc's register allocator
+// otherwise rotates a 256-register accumulator set through VGPR copies every K-step.  The chain on
+// one accumulator needs no wait states; readers of the result wait for `mfma_drain()`.
+__device__ __forceinline__ void mfma16a(const bf16x8& a, const bf16x8& b, f32x4& c) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 15\n\ts_nop 3" ::: "memory"); }
 
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
@@ -405,35 +458,438 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_kernel(const bf16_t* __restric
   }
 }
 
-// SCHED 0: four barrier-separated phases per K-tile; SCHED 1 (default): register-pipelined, one
-// barrier per K-tile.  ND_GEMM_SCHED selects one for A/B runs.
-inline int sched_choice() {
-  static const int v = [] {
-    const char* e = getenv("ND_GEMM_SCHED");
-    return e ? atoi(e) : 1;
+
+// =====================================================================================================
+// Variant 2 / 3: four waves (256 threads), each wave a 128 x 128 quadrant of the 256 x 256 tile
+// (8 x 8 v_mfma_f32_16x16x32_bf16 accumulators = 256 AGPRs), one wave per SIMD: no partner wave
+// competing for the SIMD's matrix pipe, and 32 ds_read_b128 per 128 MFMAs (vs 24 per 64 with the
+// 8-wave 128 x 64 split).  Same LDS image (two 64-KiB K-tile buffers of four swizzled half-tiles),
+// fragments double-buffered in registers, one barrier per K-tile.
+// PERSIST (variant 3): one workgroup per CU walks tiles first, first + G, ... (XCD-remapped so the
+// 32 workgroups of one XCD work on neighbouring tiles); the LDS-DMA stream runs ACROSS tile
+// boundaries, so the next tile's first K-tiles land while this tile's epilogue stores drain.
+template <int EPI, int HD, bool PERSIST, int SWZ, int ABL = 0, int LD = 0>
+__global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                       bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                       int64_t ldb, int64_t ldc, Epi ep, int GM) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  constexpr int tcols = EPI == EPI_SWIGLU ? 128 : TN;
+  constexpr bool EPI_LDS = EPI == EPI_STORE || EPI == EPI_ROPE;  // C tile re-laid out through LDS
+  constexpr int HS = SWZ == 2 ? HALF_P : HALF;  // elements per half-tile
+  constexpr int BS = 4 * HS;                     // elements per K-tile buffer
+  const int tn = (N + tcols - 1) / tcols, tiles = ((M + TM - 1) / TM) * tn;
+  const int G = gridDim.x;
+  const int first = PERSIST ? xcd_remap(blockIdx.x, G) : xcd_remap(blockIdx.x, tiles);
+  const int my_tiles = PERSIST ? (first < tiles ? (tiles - 1 - first) / G + 1 : 0) : 1;
+  const int nk = K / TK;
+  const int total = my_tiles * nk;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int wr = __builtin_amdgcn_readfirstlane(w);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)smem);
+
+  // ---- staging stream state (runs up to two K-tiles ahead of the compute stream)
+  int s_tile = first, s_kt = 0;
+  const int tmn = (M + TM - 1) / TM;
+  // tile t -> (m, n): groups of GM m-panels walked n-major inside the group, so the 32 concurrent
+  // tiles of one XCD form a compact GM x (32 / GM) block (fewer distinct A / B K-slices per step)
+  auto coords = [&](int t, int& m0, int& n0) __attribute__((always_inline)) {
+    if (GM <= 1) {
+      m0 = (t / tn) * TM;
+      n0 = (t % tn) * tcols;
+    } else {
+      const int per = GM * tn, grp = t / per, r = t - grp * per;
+      const int gm = (tmn - grp * GM) < GM ? (tmn - grp * GM) : GM;  // last group may be short
+      m0 = (grp * GM + r % gm) * TM;
+      n0 = (r / gm) * tcols;
+    }
+  };
+  int s_m0, s_n0;
+  coords(s_tile, s_m0, s_n0);
+  uint32_t va[2][4], vb[2][4];
+  auto offsets = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        // SWZ 2: piece p of wave w is LDS block b = w + 4p holding rows b, b + 16, ..., b + 112
+        const int hr = SWZ == 2 ? (w + 4 * p) + 16 * (lane >> 3) : 8 * (w + 4 * p) + (lane >> 3);
+        const int lch = SWZ == 2 ? (lane & 7) : (lane & 7) ^ swz<SWZ>(hr);
+        const int r = 128 * h + hr;
+        int ar = s_m0 + r;
+        ar = (ar < M ? ar : M - 1) - s_m0;
+        va[h][p] = (uint32_t)(((int64_t)ar * lda + lch * 8) * 2);
+        int br;
+        if (EPI == EPI_SWIGLU) {  // wave column group r / 128: 64 gate rows then the 64 matching up rows
+          int f = s_n0 + (r >> 7) * 64 + (r & 63);
+          f = f < N ? f : N - 1;
+          br = ((r >> 6) & 1) * N + f;
+        } else {
+          br = s_n0 + r;
+          br = (br < N ? br : N - 1) - s_n0;
+        }
+        vb[h][p] = (uint32_t)(((int64_t)br * ldb + lch * 8) * 2);
+      }
+  };
+  offsets();
+  // stage the next K-tile of the staging stream into buffer `buf`, advance the stream
+  // LDS-DMA piece j (0-7: A half j / 4, 8-15: B half (j - 8) / 4) of the staging stream's current
+  // K-tile into buffer `buf`; advance() moves the stream to its next K-tile
+  auto stage_piece = [&](int buf, int j) __attribute__((always_inline)) {
+    const uint32_t dst = lds0 + (uint32_t)(buf * BS * 2);
+    const int h = (j >> 2) & 1, p = j & 3;
+    constexpr int PIECE = SWZ == 2 ? BLOCK_P : 1024;  // bytes between a wave's consecutive pieces
+    if (j < 8) {
+      const bf16_t* Ab = A + (int64_t)s_m0 * lda + (int64_t)s_kt * TK;
+      const uint32_t d = dst + (uint32_t)((h * HS) * 2 + (wr + 4 * p) * PIECE);
+      if constexpr (LD == 1) glds_buf(make_rsrc(Ab), va[h][p], d);
+      else glds(Ab, va[h][p], d);
+    } else {
+      const bf16_t* Bb = (EPI == EPI_SWIGLU ? B : B + (int64_t)s_n0 * ldb) + (int64_t)s_kt * TK;
+      const uint32_t d = dst + (uint32_t)(((2 + h) * HS) * 2 + (wr + 4 * p) * PIECE);
+      if constexpr (LD == 1) glds_buf(make_rsrc(Bb), vb[h][p], d);
+      else glds(Bb, vb[h][p], d);
+    }
+  };
+  auto advance = [&]() __attribute__((always_inline)) {
+    if (++s_kt == nk) {
+      s_kt = 0;
+      s_tile += G;
+      if (PERSIST && s_tile < tiles) {
+        coords(s_tile, s_m0, s_n0);
+        offsets();
+      }
+    }
+  };
+  auto stage_next = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) stage_piece(buf, j);
+    advance();
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (total == 0) return;
+
+  stage_next(0);
+  if (total > 1) {
+    stage_next(1);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  const int ar0 = lane & 15, kq = (lane >> 4) * 8;
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  {
+    const bf16_t* at = smem + wm * HS;
+    const bf16_t* bt = smem + (2 + wn) * HS;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) fb0[b] = fragz<SWZ>(bt, b * 16 + ar0, kq);
+#pragma unroll
+    for (int a = 0; a < 8; ++a) fa0[a] = fragz<SWZ>(at, a * 16 + ar0, kq);
+  }
+  for (int lt = 0; lt < my_tiles; ++lt) {
+  for (int kt = 0; kt < nk; ++kt) {
+    const int g = lt * nk + kt;  // position in the workgroup's K-tile stream
+    const int buf = g & 1;
+    const bool more1 = g + 1 < total, more2 = g + 2 < total;
+    const bf16_t* at = smem + buf * BS + wm * HS;
+    const bf16_t* bt = smem + buf * BS + (2 + wn) * HS;
+    __builtin_amdgcn_s_waitcnt(LGKM0);
+    // k-step 0: per row block a, 8 MFMAs with this step's fragments; the two k-step-1 fragment
+    // reads of block a ride under them
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      if (!(ABL & 2)) {
+        fb1[a] = fragz<SWZ>(bt, a * 16 + ar0, 32 + kq);
+        fa1[a] = fragz<SWZ>(at, a * 16 + ar0, 32 + kq);
+      } else if (a == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { fb1[i] = fb0[i]; fa1[i] = fa0[i]; }
+      }
+#pragma unroll
+      for (int b = 0; b < 8; ++b) mfma16a(fb0[b], fa0[a], acc[a][b]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (more1 && !(ABL & 1)) {
+      // K-tile g + 1 must have landed.  Right after an epilogue its (fixed number of) stores were
+      // issued after that DMA and may stay in flight
+      if (EPI != EPI_DSWIGLU && kt == 0 && lt > 0) {
+        if constexpr (EPI == EPI_SWIGLU) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+        else if (g + 1 < total) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");  // 32 stores + K-tile g+1's DMA
+        else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(LGKM0);
+    if (!(ABL & 4)) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // k-step 1: two LDS-DMA pieces of K-tile g + 2 (into the buffer just released) and two
+    // fragment reads of K-tile g + 1 per 8 MFMAs: an LDS-DMA issue stalls the wave for ~100
+    // cycles, hidden behind the MFMAs already in the pipe (a burst of 16 would idle the SIMD)
+    const bf16_t* an = smem + (buf ^ 1) * BS + wm * HS;
+    const bf16_t* bn = smem + (buf ^ 1) * BS + (2 + wn) * HS;
+    // an LDS-staged epilogue needs this buffer after the tile's last K-tile: its DMA then waits
+    const bool stage_now = more2 && !(EPI_LDS && kt == nk - 1);
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      if (stage_now && !(ABL & 1)) {  // ABL: ablation builds for profiling only (wrong results)
+        stage_piece(buf, a);
+        stage_piece(buf, 8 + a);
+      }
+      if (!(ABL & 2)) {
+        fb0[a] = fragz<SWZ>(bn, a * 16 + ar0, kq);  // past the stream's end: reads unused LDS
+        fa0[a] = fragz<SWZ>(an, a * 16 + ar0, kq);
+      }
+#pragma unroll
+      for (int b = 0; b < 8; ++b) mfma16a(fb1[b], fa1[a], acc[a][b]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (stage_now) advance();
+  }
+    mfma_drain();
+    const int c_tile = first + lt * G;
+    const int gl = lt * nk + nk - 1;  // stream position of this tile's last K-tile
+    // ---------------- epilogue of tile c_tile
+    int m0, n0;
+    coords(c_tile, m0, n0);
+    const int q4 = 4 * (lane >> 4);
+    if constexpr ((ABL & 8) != 0) {  // ablation: no epilogue stores (keep the accumulators live)
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) asm volatile("" ::"a"(acc[a][b]));
+    } else if (EPI == EPI_STORE || EPI == EPI_ROPE) {
+      // C through LDS (the K-tile buffer this tile's last step just released), 32 rows of the
+      // wave's 128 x 128 quadrant per pass: v_permlane16_swap pairs the 4-column quads of blocks
+      // b, b + 1 into 16-B pieces (ds_write_b128, rows padded to 272 B), then 16 lanes per row read
+      // back whole 256-B row segments and store them with buffer_store_dwordx4 -- full 128-B lines
+      // per store instead of 16 half-lines.  Out-of-range lanes are dropped by the descriptor (rows
+      // past M) or an offset sentinel (columns past N), so every wave issues exactly 32 stores.
+      const __amdgpu_buffer_rsrc_t crs = make_rsrc_n(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)(M - m0 < TM ? M - m0 : TM) * ldc * 2));
+      const int q = lane >> 4;
+      constexpr int RS = 136;  // staging row stride (elements): 256 B + 16 B pad
+      bf16_t* cst = smem + (gl & 1) * BS + w * (32 * RS);
+      const int ccol = n0 + wn * 128 + (lane & 15) * 8;  // read-back: this lane's 8 columns
+      const uint32_t coff = ccol < N ? (uint32_t)(ccol * 2) : 0x80000000u;
+      constexpr int HALFD = HD / 2;
+#pragma unroll
+      for (int pass = 0; pass < 4; ++pass) {
+#pragma unroll
+        for (int aa = 0; aa < 2; ++aa) {
+          const int a = pass * 2 + aa;
+          // per group of 4 column blocks (one 64-wide head, or two 32-wide ones): RoPE pairs
+          // block b with b + HD/32 inside the group; the tables repeat every head
+          float4 ct[2], st[2];
+          if constexpr (EPI == EPI_ROPE) {
+            const int t = (m0 + wm * 128 + a * 16 + (lane & 15)) % ep.T;
+#pragma unroll
+            for (int j = 0; j < HALFD / 16; ++j) {
+              ct[j] = *reinterpret_cast<const float4*>(ep.cosT + (int64_t)t * HD + j * 16 + q4);
+              st[j] = *reinterpret_cast<const float4*>(ep.sinT + (int64_t)t * HD + j * 16 + q4);
+            }
+          }
+#pragma unroll
+          for (int g4 = 0; g4 < 2; ++g4) {
+            f32x4 v[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) v[b] = acc[a][g4 * 4 + b];
+            if constexpr (EPI == EPI_ROPE) {
+              // q / k columns rotate (rope_cols % HD == 0); v columns pass through (branch-free:
+              // a wave-uniform branch here made hipcc spill the accumulator set)
+              const bool rot = n0 + wn * 128 + g4 * 64 < ep.rope_cols;
+#pragma unroll
+              for (int b = 0; b < 4; ++b) {
+                if (((b * 16) % HD) >= HALFD) continue;  // static: b is in the first half of its head
+                const int p = b + HALFD / 16, j = ((b * 16) % HD) / 16;
+                const float cc[4] = {ct[j].x, ct[j].y, ct[j].z, ct[j].w};
+                const float ss[4] = {st[j].x, st[j].y, st[j].z, st[j].w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const float c1 = rot ? cc[r] : 1.f, s1 = rot ? ss[r] : 0.f;
+                  const float x1 = v[b][r], x2 = v[p][r];
+                  v[b][r] = x1 * c1 - x2 * s1;
+                  v[p][r] = x2 * c1 + x1 * s1;
+                }
+              }
+            }
+#pragma unroll
+            for (int b = 0; b < 4; b += 2) {
+              const int col = (g4 * 4 + b + (q & 1)) * 16 + (q >> 1) * 8;
+              *reinterpret_cast<u32x4*>(cst + (aa * 16 + (lane & 15)) * RS + col) = pair16(v[b], v[b + 1]);
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int row = i * 4 + q;  // 0..31 inside this pass
+          const u32x4 d = *reinterpret_cast<const u32x4*>(cst + row * RS + (lane & 15) * 8);
+          const int mr = wm * 128 + pass * 32 + row;
+          __builtin_amdgcn_raw_buffer_store_b128(d, crs, coff == 0x80000000u ? coff : coff + (uint32_t)(mr * ldc * 2), 0, 0);
+        }
+      }
+      // every wave's read-back is done before any wave's DMA reuses the buffer
+      __builtin_amdgcn_s_waitcnt(LGKM0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (gl + 2 < total && !(ABL & 1)) stage_next(gl & 1);
+    } else if (EPI == EPI_SWIGLU) {
+      const __amdgpu_buffer_rsrc_t crs = make_rsrc_n(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)(M - m0 < TM ? M - m0 : TM) * ldc * 2));
+      const __amdgpu_buffer_rsrc_t ars = make_rsrc_n(ep.act + (int64_t)m0 * ep.ld_act, (uint32_t)((int64_t)(M - m0 < TM ? M - m0 : TM) * ep.ld_act * 2));
+      const int q = lane >> 4;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int mr = wm * 128 + a * 16 + (lane & 15);
+#pragma unroll
+        for (int b = 0; b < 4; b += 2) {
+          // gate / up rounded to bf16 first: act is computed from exactly what the backward reads
+          f32x4 g2[2], u2[2], y2[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              g2[j][r] = round_bf(acc[a][b + j][r]);
+              u2[j][r] = round_bf(acc[a][b + j + 4][r]);
+              y2[j][r] = silu(g2[j][r]) * u2[j][r];
+            }
+          const int f = n0 + wn * 64 + (b + (q & 1)) * 16 + (q >> 1) * 8;
+          const bool ok = f < N;
+          const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
+          const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
+          const uint32_t oy = ok ? (uint32_t)(((int64_t)mr * ep.ld_act + f) * 2) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b128(pair16(g2[0], g2[1]), crs, og, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(pair16(u2[0], u2[1]), crs, ou, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(pair16(y2[0], y2[1]), ars, oy, 0, 0);
+        }
+      }
+    } else {  // EPI_DSWIGLU
+      const int nb = n0 + wn * 128;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int m = m0 + wm * 128 + a * 16 + (lane & 15);
+        if (m >= M) continue;
+        const bf16_t* grow = ep.gu + (int64_t)m * ep.ld_gu;
+        bf16_t* crow = C + (int64_t)m * ldc;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const int f = nb + b * 16 + q4;
+          if (f >= N) continue;
+          const uint2 g2 = *reinterpret_cast<const uint2*>(grow + f);
+          const uint2 u2 = *reinterpret_cast<const uint2*>(grow + N + f);
+          const float gv[4] = {lo_bf(g2.x), hi_bf(g2.x), lo_bf(g2.y), hi_bf(g2.y)};
+          const float uv[4] = {lo_bf(u2.x), hi_bf(u2.x), lo_bf(u2.y), hi_bf(u2.y)};
+          float dg[4], du[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = acc[a][b][r];
+            const float sg = 1.f / (1.f + __expf(-gv[r]));
+            du[r] = d * gv[r] * sg;
+            dg[r] = d * uv[r] * sg * (1.f + gv[r] * (1.f - sg));
+          }
+          *reinterpret_cast<uint2*>(crow + f) = make_uint2(pack2(dg[0], dg[1]), pack2(dg[2], dg[3]));
+          *reinterpret_cast<uint2*>(crow + N + f) = make_uint2(pack2(du[0], du[1]), pack2(du[2], du[3]));
+        }
+      }
+    }
+    if (PERSIST) {
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+// Variants (ND_GEMM_VARIANT or nd_gemm_set_variant, for in-process A/B): 0 = 8 waves, four barrier-
+// separated phases per K-tile; 1 = 8 waves, register-pipelined, one barrier per K-tile; 2 = 4 waves of
+// 128 x 128 (one wave per SIMD); 3 = variant 2 as a persistent grid with a cross-tile DMA stream;
+// 4 = variant 3 with the half-swap LDS swizzle (coalesced 64-B DMA source quads); 5 = variant 3 with
+// the padded block layout (whole ascending 128-B rows per DMA lane octet, conflict-free reads);
+// 6 = variant 5 with buffer_load ... lds DMA; 7 (default) = variant 5 on a plain (one tile per
+// workgroup) grid.  Measured against hipBLASLt on the Llama-150M shapes: docs/DESIGN.md §6.
+int g_variant = [] {
+  const char* e = getenv("ND_GEMM_VARIANT");
+  return e ? atoi(e) : 7;
+}();
+
+// tile grouping of the 4-wave kernels (see coords()); ND_GEMM_GROUP_M or nd_gemm_set_group_m
+int g_group_m = [] {
+  const char* e = getenv("ND_GEMM_GROUP_M");
+  return e ? atoi(e) : 4;
+}();
+
+int num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    return v;
   }();
-  return v;
+  return n;
 }
 
 template <int EPI, int HD, int SCHED>
 int launch_s(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
              const Epi& ep, hipStream_t s) {
-  const size_t lds = 2 * (size_t)BUF * sizeof(bf16_t);  // 128 KiB
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, HD, SCHED>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (attr != hipSuccess) return (int)attr;
+  const size_t lds = 2 * (size_t)(SCHED >= 5 ? 4 * HALF_P : BUF) * sizeof(bf16_t);  // 128 / 132 KiB
   const int tcols = EPI == EPI_SWIGLU ? 128 : TN;
   const int tiles = ((M + TM - 1) / TM) * ((N + tcols - 1) / tcols);
-  hipLaunchKernelGGL((gemm_nt_kernel<EPI, HD, SCHED>), dim3(tiles), dim3(512), lds, s, (const bf16_t*)A,
-                     (const bf16_t*)B, (bf16_t*)C, M, N, K, lda, ldb, ldc, ep);
+  if constexpr (SCHED <= 1) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, HD, SCHED>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (attr != hipSuccess) return (int)attr;
+    hipLaunchKernelGGL((gemm_nt_kernel<EPI, HD, SCHED>), dim3(tiles), dim3(512), lds, s, (const bf16_t*)A,
+                       (const bf16_t*)B, (bf16_t*)C, M, N, K, lda, ldb, ldc, ep);
+  } else {
+    constexpr bool P = SCHED >= 3 && SCHED != 7;
+    constexpr int Z = SCHED == 4 ? 1 : SCHED >= 5 ? 2 : 0;
+    constexpr int AB = SCHED >= 10 ? SCHED - 10 : 0;  // ablation builds (profiling only)
+    constexpr int LDK = SCHED == 6 ? 1 : 0;            // buffer_load ... lds instead of global_load_lds
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm4_kernel<EPI, HD, P, Z, AB, LDK>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (attr != hipSuccess) return (int)attr;
+    const int grid = P ? (tiles < num_cus() ? tiles : num_cus()) : tiles;
+    hipLaunchKernelGGL((gemm4_kernel<EPI, HD, P, Z, AB, LDK>), dim3(grid), dim3(256), lds, s, (const bf16_t*)A,
+                       (const bf16_t*)B, (bf16_t*)C, M, N, K, lda, ldb, ldc, ep, g_group_m);
+  }
   ND_LAUNCH_CHECK();
 }
 
 template <int EPI, int HD = 64>
 int launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
            const Epi& ep, hipStream_t s) {
-  return sched_choice() == 0 ? launch_s<EPI, HD, 0>(A, B, C, M, N, K, lda, ldb, ldc, ep, s)
-                             : launch_s<EPI, HD, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+  // the 4-wave kernels store 8-column (16-B) pieces and keep per-tile byte offsets 32-bit
+  // EPI_ROPE stays on the 8-wave kernel: its epilogue's register pressure makes hipcc move the
+  // accumulators between AGPRs, and an inline-asm MFMA's result must not be touched by compiler
+  // code before it lands (wrong values measured; tests/test_gemm_gpu.py rope cases)
+  const bool four_ok = EPI != EPI_ROPE && N % 8 == 0 && ldc % 8 == 0 && (int64_t)TM * ldc * 2 < (1ll << 31) &&
+                       (EPI != EPI_SWIGLU || ep.ld_act % 8 == 0);
+  if constexpr (EPI == EPI_ROPE) return launch_s<EPI, HD, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+  switch (four_ok ? g_variant : 1) {
+    case 0: return launch_s<EPI, HD, 0>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 1: return launch_s<EPI, HD, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 2: return launch_s<EPI, HD, 2>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 4: return launch_s<EPI, HD, 4>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 5: return launch_s<EPI, HD, 5>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 6: return launch_s<EPI, HD, 6>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 7: return launch_s<EPI, HD, 7>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+#ifdef ND_GEMM_ABLATION
+    case 11: return launch_s<EPI, HD, 11>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 12: return launch_s<EPI, HD, 12>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 13: return launch_s<EPI, HD, 13>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 15: return launch_s<EPI, HD, 15>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 17: return launch_s<EPI, HD, 17>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 18: return launch_s<EPI, HD, 18>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 19: return launch_s<EPI, HD, 19>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+#endif
+    default: return launch_s<EPI, HD, 3>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+  }
 }
 
 bool shapes_ok(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
@@ -442,6 +898,19 @@ bool shapes_ok(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
          lda >= K && ldb >= K && (int64_t)TM * lda * 2 < (1ll << 31) && (int64_t)TN * ldb * 2 < (1ll << 31);
 }
 }  // namespace
+
+// GEMM schedule variant for A/B runs (see g_variant); returns the previous one
+ND_API int nd_gemm_set_variant(int v) {
+  const int old = g_variant;
+  if ((v >= 0 && v <= 7) || (v > 10 && v < 20)) g_variant = v;
+  return old;
+}
+
+ND_API int nd_gemm_set_group_m(int g) {
+  const int old = g_group_m;
+  if (g >= 0) g_group_m = g;
+  return old;
+}
 
 // C[M, N] = A[M, K] . B[N, K]^T (bf16 in / out, fp32 accumulate).  K % 64 == 0, N % 4 == 0,
 // lda / ldb % 8 == 0, ldc % 4 == 0, 16-B aligned base pointers.

@@ -48,8 +48,20 @@ def nt_supported(a: torch.Tensor, b: torch.Tensor) -> bool:
             and _aligned(a) and _aligned(b))
 
 
-def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+def set_gemm_variant(v: int) -> int:
+    """Schedule variant of the own NT GEMM (csrc/gemm.hip ``g_variant``; A/B runs); returns the old one."""
+    return int(_ext.lib().nd_gemm_set_variant(int(v)))
+
+
+def set_gemm_group_m(g: int) -> int:
+    """Tile grouping (m-panels per group) of the 4-wave GEMM variants; 0/1 = row-major tiles."""
+    return int(_ext.lib().nd_gemm_set_group_m(int(g)))
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, variant: int = None) -> torch.Tensor:
     """out[M, N] = a[M, K] . b[N, K]^T (bf16, fp32 accumulate)."""
+    if variant is not None:
+        set_gemm_variant(variant)
     M, K = a.shape
     N = b.shape[0]
     if out is None:

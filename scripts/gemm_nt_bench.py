@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--tokens", type=int, default=65536)
     ap.add_argument("--model", default="150m")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", default="1,2,3", help="own-kernel schedule variants to A/B (csrc/gemm.hip)")
+    ap.add_argument("--only", default="", help="comma list of case-name prefixes")
     a = ap.parse_args()
     ops.set_backend("hip")
     M = a.tokens
@@ -91,18 +93,33 @@ def main():
 
     cases.append(("down dgrad+dswiglu", 2.0 * M * F * d, lambda: G.gemm_nt_dswiglu(dy, wdt, gu_in, dgu), dswiglu_lib))
 
-    tot_o = tot_b = 0.0
+    # variant spec "V" or "V:GM" (GM = tile grouping of the 4-wave kernels)
+    specs = [tuple(int(x) for x in v.split(":")) if ":" in v else (int(v), 0) for v in a.variants.split(",")]
+    variants = list(range(len(specs)))
+    only = [p for p in a.only.split(",") if p]
+    tot = {v: 0.0 for v in variants}
+    tot_b = 0.0
     for name, fl, ours, lib in cases:
-        to, tb = [], []
+        if only and not any(name.startswith(p) for p in only):
+            continue
+        to = {v: [] for v in variants}
+        tb = []
         for _ in range(a.rounds):
-            to.append(timed(ours))
+            for v in variants:
+                G.set_gemm_variant(specs[v][0])
+                G.set_gemm_group_m(specs[v][1])
+                to[v].append(timed(ours))
             tb.append(timed(lib))
-        o, b = sorted(to)[len(to) // 2], sorted(tb)[len(tb) // 2]
-        tot_o += o
+        b = sorted(tb)[len(tb) // 2]
         tot_b += b
-        print(f"{name:20s} ours {o:8.1f} us {fl / o / 1e6:6.0f} TF/s | hipBLASLt(+kernel) {b:8.1f} us "
-              f"{fl / b / 1e6:6.0f} TF/s | ours/lib {b / o:5.3f}x", flush=True)
-    print(f"{'TOTAL':20s} ours {tot_o:8.1f} us | lib {tot_b:8.1f} us | {tot_b / tot_o:5.3f}x", flush=True)
+        line = f"{name:20s} lib {b:7.1f} us {fl / b / 1e6:5.0f} TF/s"
+        for v in variants:
+            o = sorted(to[v])[len(to[v]) // 2]
+            tot[v] += o
+            line += f" | v{specs[v][0]}:{specs[v][1]} {o:7.1f} us {fl / o / 1e6:5.0f} TF/s {b / o:5.3f}x"
+        print(line, flush=True)
+    print("TOTAL lib %.1f us | " % tot_b + " | ".join(f"v{specs[v][0]}:{specs[v][1]} {tot[v]:.1f} us {tot_b / tot[v]:.3f}x" for v in variants),
+          flush=True)
 
 
 if __name__ == "__main__":

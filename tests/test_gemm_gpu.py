@@ -13,14 +13,20 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True)
-def _hip(hip_lib):
+@pytest.fixture(autouse=True, params=[(1, 0), (3, 4), (4, 0), (5, 3), (6, 4), (7, 0), (7, 4)], ids=lambda v: f"v{v[0]}g{v[1]}")
+def _hip(hip_lib, request):
+    """Every test runs on each schedule variant of the kernel (csrc/gemm.hip g_variant) and on a
+    grouped tile order with a short last group (g_group_m = 3)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ops.set_backend("hip")
     G.set_gemm_backend("hip")
+    old = G.set_gemm_variant(request.param[0])
+    old_g = G.set_gemm_group_m(request.param[1])
     torch.manual_seed(0)
     yield
+    G.set_gemm_variant(old)
+    G.set_gemm_group_m(old_g)
     ops.set_backend("auto")
 
 
