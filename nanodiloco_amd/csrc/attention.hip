@@ -326,7 +326,8 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int nh, int nkv, int T,
                                                           int64_t ld, int64_t ldo, float scale,
-                                                          const float* __restrict__ cosT, const float* __restrict__ sinT) {
+                                                          const float* __restrict__ cosT, const float* __restrict__ sinT,
+                                                          const int* __restrict__ KS) {
   constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * BN * HD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * BN * HD];
@@ -335,6 +336,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
   const int qb = nqb - 1 - (int)(blockIdx.x / bh_count);  // longest causal rows first
   const int bh = blockIdx.x % bh_count;
   const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
+  const int ks = KS ? KS[b] : 0;  // left padding: keys < ks are masked for the real queries (>= ks)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15;
   const int q0w = qb * 128 + w * 32, qi = q0w + c32;
@@ -402,13 +404,13 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
 #pragma unroll
         for (int t = 0; t < NT; ++t) s[kt] = mfma32(ka[kt][t], qf[t], s[kt]);
       }
-      if ((k0 + BN - 1 > q0w) || (k0 + BN > T)) {
+      if ((k0 + BN - 1 > q0w) || (k0 + BN > T) || (k0 < ks)) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (key > qi || key >= T) s[kt][r] = -INFINITY;
+            if (key > qi || key >= T || key < ks) s[kt][r] = -INFINITY;
           }
       }
       float mx = -INFINITY;
@@ -418,14 +420,16 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
       mx = pair_max32(mx) * c;  // raw-score max -> log2 domain (c > 0)
       const float mnew = fmaxf(m, mx);
-      const float alpha = fexp2(m - mnew);
+      // a row with no visible key yet (a left-pad query: every key masked) keeps p = 0, l = 0
+      const float mref = mnew == -INFINITY ? 0.f : mnew;
+      const float alpha = fexp2(m - mref);
       m = mnew;
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = fexp2(fmaf(s[kt][r], c, -mnew));
+          const float p = fexp2(fmaf(s[kt][r], c, -mref));
           s[kt][r] = p;
           rs += p;
         }
@@ -508,7 +512,8 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
                                                              const float* __restrict__ cosT, const float* __restrict__ sinT,
                                                              const bf16_t* __restrict__ O = nullptr,
                                                              float* __restrict__ NL = nullptr,
-                                                             float* __restrict__ ND = nullptr) {
+                                                             float* __restrict__ ND = nullptr,
+                                                             const int* __restrict__ KS = nullptr) {
   constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * BN * HD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * BN * HD];
@@ -517,6 +522,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
   const int qb = nqb - 1 - (int)(blockIdx.x / bh_count);
   const int bh = blockIdx.x % bh_count;
   const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
+  const int ks = KS ? KS[b] : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15;
   const int q0w = qb * 128 + w * 32, qi = q0w + c32;
@@ -593,7 +599,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
       if (j + 1 < ntiles) dma_issue(j + 1);
     }
     if (k0 <= q0w + 31) {
-      const bool diag = (k0 + BN - 1 > q0w) || (k0 + BN > T) || (qi >= T);
+      const bool diag = (k0 + BN - 1 > q0w) || (k0 + BN > T) || (qi >= T) || (k0 < ks);
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         if (k0 + kt * 32 > q0w + 31) continue;  // this 32-key half is above the wave's diagonal
@@ -621,7 +627,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const float p = (key <= qi && key < T && qi < T) ? fexp2(fmaf(s[r], c, -lse)) : 0.f;
+            const float p = (key <= qi && key < T && qi < T && key >= ks) ? fexp2(fmaf(s[r], c, -lse)) : 0.f;
             dp[r] = p * (dp[r] - dlt);
           }
         }
@@ -659,7 +665,8 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
                                                                bf16_t* __restrict__ dV, int B, int nh, int nkv, int T,
                                                                int64_t ld, int64_t ldo, float scale,
                                                                const float* __restrict__ cosT,
-                                                               const float* __restrict__ sinT) {
+                                                               const float* __restrict__ sinT,
+                                                               const int* __restrict__ KS) {
   constexpr int BQ = 64, NT = HD / 16, NO = HD / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Qs[2 * BQ * HD];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[2 * BQ * HD];
@@ -670,6 +677,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
   const int kb = (int)(blockIdx.x / bk_count);  // small kb = longest query range: dispatched first
   const int bk = blockIdx.x % bk_count;
   const int b = bk / nkv, kvh = bk % nkv;
+  const int ks = KS ? KS[b] : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15;
   const int kw0 = kb * 128 + w * 32, key = kw0 + c32;
@@ -761,7 +769,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
         s = mfma32(qa[t], kf[t], s);
         dp = mfma32(da[t], vf[t], dp);
       }
-      const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T);
+      const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T) || (kw0 < ks);
       if (!diag) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -773,7 +781,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qq = qsub + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float p = (key <= qq && qq < T && key < T) ? fexp2(s[r] * c) : 0.f;
+          const float p = (key <= qq && qq < T && key < T && key >= ks) ? fexp2(s[r] * c) : 0.f;
           s[r] = p;
           dp[r] = p * dp[r];
         }
@@ -802,33 +810,43 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
 // ------------------------------------------------------------------------------------ launchers
 template <int HD>
 static int fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, int B, int nh, int nkv, int T,
-                      int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, hipStream_t s) {
+                      int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, const int* ks,
+                      hipStream_t s) {
   const int nqb = (T + 127) / 128;
   const dim3 g(nqb * B * nh), b(256);
   if (cosT)
     hipLaunchKernelGGL((attn_fwd_kernel<HD, true>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                       (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+                       (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   else if (T % 64 == 0 && !(getenv("ND_ATTN_FWD") && getenv("ND_ATTN_FWD")[0] == 'r'))
     hipLaunchKernelGGL((attn_fwd_kernel<HD, false, true>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+                       (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   else
     hipLaunchKernelGGL((attn_fwd_kernel<HD, false>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                       (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+                       (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   ND_LAUNCH_CHECK();
 }
 
 // cosT/sinT: fp32 [T, hd] RoPE tables (nullptr = q/k already rotated).  q/k/v are then the RAW
 // projection outputs and the kernel rotates q and k on load.
+// ks: per-sequence key start [B] (int32, device; nullptr = none) for left-padded batches: query q
+// attends to keys ks[b] <= k <= q -- HF's causal & padding mask.  A pad query (q < ks[b]) sees no key
+// and outputs 0 (what torch SDPA returns for a fully masked row, i.e. the reference's HF model).
+ND_API int nd_attn_fwd_ks(const void* q, const void* k, const void* v, void* o, float* lse, int B, int nh, int nkv,
+                          int T, int hd, int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale,
+                          const int* ks, hipStream_t s) {
+  if (nh % nkv || (ld % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
+  switch (hd) {
+    case 32: return fwd_launch<32>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
+    case 64: return fwd_launch<64>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
+    case 128: return fwd_launch<128>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
 ND_API int nd_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int nh, int nkv, int T,
                        int hd, int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale,
                        hipStream_t s) {
-  if (nh % nkv || (ld % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
-  switch (hd) {
-    case 32: return fwd_launch<32>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
-    case 64: return fwd_launch<64>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
-    case 128: return fwd_launch<128>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
-    default: return (int)hipErrorInvalidValue;
-  }
+  return nd_attn_fwd_ks(q, k, v, o, lse, B, nh, nkv, T, hd, ld, ldo, cosT, sinT, scale, nullptr, s);
 }
 
 ND_API int nd_attn_bwd_pre(const void* o, const void* dout, float* delta, int B, int nh, int T, int64_t hd,
@@ -866,7 +884,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ NL, const float* __restrict__ ND, bf16_t* __restrict__ dK,
     bf16_t* __restrict__ dV, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
-    const float* __restrict__ cosT, const float* __restrict__ sinT) {
+    const float* __restrict__ cosT, const float* __restrict__ sinT, const int* __restrict__ KS) {
   constexpr int NT = HD / 16, NO = HD / 32;
   constexpr int CPR = HD / 8;              // 16-B chunks per row
   constexpr int RPI = 64 / CPR;            // rows per 1-KiB DMA wave-instruction
@@ -880,6 +898,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
   const int kb = (int)(blockIdx.x / bk_count);
   const int bk = blockIdx.x % bk_count;
   const int b = bk / nkv, kvh = bk % nkv;
+  const int ks = KS ? KS[b] : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15;
   const int kw0 = kb * 128 + w * 32, key = kw0 + c32;
@@ -977,7 +996,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
         s = mfma32(qa[t], kf[t], s);
         dp = mfma32(da[t], vf[t], dp);
       }
-      const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T);
+      const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T) || (kw0 < ks);
       if (!diag) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -989,7 +1008,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qq = qsub + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float p = (key <= qq && qq < T && key < T) ? fexp2(s[r] * c) : 0.f;
+          const float p = (key <= qq && qq < T && key < T && key >= ks) ? fexp2(s[r] * c) : 0.f;
           s[r] = p;
           dp[r] = p * dp[r];
         }
@@ -1015,7 +1034,8 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
 template <int HD, bool ROPE, bool ROPE_OUT>
 static void bwd_launch_t(const void* q, const void* k, const void* v, const void* dout, const float* lse,
                          const float* delta, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T,
-                         int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, hipStream_t s) {
+                         int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, const int* ks,
+                         hipStream_t s) {
   const int nb = (T + 127) / 128;
   const char* ev = getenv("ND_ATTN_DKDV");
   const bool dma = !ROPE && ws != nullptr && T % 64 == 0 && !(ev && ev[0] == 'r');
@@ -1028,24 +1048,24 @@ static void bwd_launch_t(const void* q, const void* k, const void* v, const void
     if (!(bq && bq[0] == '6') && T % 128 == 0)
       hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128>), dim3(nb * B * nkv), dim3(256), 0, s,
                          (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
-                         (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+                         (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
     else
       hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
                          (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
-                         (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+                         (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   } else {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, ROPE, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,
-                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   }
   if (dma)
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT, !ROPE>), dim3(nb * B * nh), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,
-                       (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+                       (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, nullptr, nullptr, nullptr, ks);
   else
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT>), dim3(nb * B * nh), dim3(256), 0, s, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, nh, nkv,
-                       T, ld, ldo, scale, cosT, sinT);
+                       T, ld, ldo, scale, cosT, sinT, nullptr, nullptr, nullptr, ks);
 }
 
 // rope_mode 0: no RoPE; 1: q/k are RAW projections -- rotated on load, dq/dk un-rotated on store;
@@ -1053,29 +1073,37 @@ static void bwd_launch_t(const void* q, const void* k, const void* v, const void
 template <int HD>
 static int bwd_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse, const float* delta,
                       void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo,
-                      const float* cosT, const float* sinT, float scale, int rope_mode, hipStream_t s) {
+                      const float* cosT, const float* sinT, float scale, int rope_mode, const int* ks, hipStream_t s) {
   if (rope_mode == 1)
-    bwd_launch_t<HD, true, true>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
+    bwd_launch_t<HD, true, true>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
   else if (rope_mode == 2)
-    bwd_launch_t<HD, false, true>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
+    bwd_launch_t<HD, false, true>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
   else
-    bwd_launch_t<HD, false, false>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, s);
+    bwd_launch_t<HD, false, false>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
   ND_LAUNCH_CHECK();
 }
 
-// dq/dk/dv may point into one packed dqkv buffer (row stride ld).
+// dq/dk/dv may point into one packed dqkv buffer (row stride ld).  ks: see nd_attn_fwd_ks.
+ND_API int nd_attn_bwd_ks(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                          const float* delta, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv,
+                          int T, int hd, int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale,
+                          int rope_mode, const int* ks, hipStream_t s) {
+  if (nh % nkv || (ld % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
+  if (rope_mode && !(cosT && sinT)) return (int)hipErrorInvalidValue;
+  switch (hd) {
+    case 32: return bwd_launch<32>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, ks, s);
+    case 64: return bwd_launch<64>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, ks, s);
+    case 128: return bwd_launch<128>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, ks, s);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
 ND_API int nd_attn_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
                        const float* delta, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv,
                        int T, int hd, int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale,
                        int rope_mode, hipStream_t s) {
-  if (nh % nkv || (ld % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
-  if (rope_mode && !(cosT && sinT)) return (int)hipErrorInvalidValue;
-  switch (hd) {
-    case 32: return bwd_launch<32>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
-    case 64: return bwd_launch<64>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
-    case 128: return bwd_launch<128>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, rope_mode, s);
-    default: return (int)hipErrorInvalidValue;
-  }
+  return nd_attn_bwd_ks(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, hd, ld, ldo, cosT, sinT, scale,
+                        rope_mode, nullptr, s);
 }
 
 // Backward with the row statistics fused into the dQ kernel (PRE): dQ (writes -delta, -LSE/c into
@@ -1084,41 +1112,50 @@ ND_API int nd_attn_bwd(const void* q, const void* k, const void* v, const void* 
 template <int HD, bool ROPE_OUT>
 static int bwd_fused_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
                             const float* lse, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T,
-                            int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, hipStream_t s) {
+                            int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, const int* ks,
+                            hipStream_t s) {
   const int nb = (T + 127) / 128;
   const int64_t n = (int64_t)B * nh * T;
   float *nl = ws, *nd = ws + n;
   hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, ROPE_OUT, true, true>), dim3(nb * B * nh), dim3(256), 0, s,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
-                     (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd);
+                     (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks);
   if (T % 128 == 0)
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
-                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   else
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
-                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT);
+                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   ND_LAUNCH_CHECK();
 }
 
-ND_API int nd_attn_bwd_fused(const void* q, const void* k, const void* v, const void* o, const void* dout,
-                             const float* lse, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T,
-                             int hd, int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale,
-                             int rope_mode, hipStream_t s) {
+ND_API int nd_attn_bwd_fused_ks(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                const float* lse, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv,
+                                int T, int hd, int64_t ld, int64_t ldo, const float* cosT, const float* sinT,
+                                float scale, int rope_mode, const int* ks, hipStream_t s) {
   if (nh % nkv || (ld % 8) || (ldo % 8) || T % 64 || ws == nullptr || rope_mode == 1) return (int)hipErrorInvalidValue;
   if (rope_mode == 2 && !(cosT && sinT)) return (int)hipErrorInvalidValue;
   switch (hd) {
 #define ND_BF(H)                                                                                               \
   case H:                                                                                                      \
     return rope_mode == 2 ? bwd_fused_launch<H, true>(q, k, v, o, dout, lse, dq, dk, dv, ws, B, nh, nkv, T, ld, \
-                                                      ldo, cosT, sinT, scale, s)                               \
+                                                      ldo, cosT, sinT, scale, ks, s)                           \
                           : bwd_fused_launch<H, false>(q, k, v, o, dout, lse, dq, dk, dv, ws, B, nh, nkv, T, ld, \
-                                                       ldo, cosT, sinT, scale, s);
+                                                       ldo, cosT, sinT, scale, ks, s);
     ND_BF(32)
     ND_BF(64)
     ND_BF(128)
 #undef ND_BF
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+ND_API int nd_attn_bwd_fused(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                             const float* lse, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T,
+                             int hd, int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale,
+                             int rope_mode, hipStream_t s) {
+  return nd_attn_bwd_fused_ks(q, k, v, o, dout, lse, dq, dk, dv, ws, B, nh, nkv, T, hd, ld, ldo, cosT, sinT, scale,
+                              rope_mode, nullptr, s);
 }

@@ -180,7 +180,7 @@ class LlamaForCausalLM:
             return None
         return self.fp8.dy_target(key) if grad else self.fp8.x_target(key)
 
-    def _layer(self, i, h, y, cos, sin, B, T, next_norm, y8=None):
+    def _layer(self, i, h, y, cos, sin, B, T, next_norm, y8=None, kstart=None):
         c = self.config
         p = f"model.layers.{i}."
         cdt = self.compute_dtype
@@ -188,7 +188,7 @@ class LlamaForCausalLM:
         qn = self._qkv_names[i]
         qkv = self._linear(f"{i}.qkv", y, self._fused(qn, "shadow"), self._fused(qn, "grad"), y8)
         o = ops.attention(qkv, cos, sin, B, T, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
-                          inplace=True)
+                          inplace=True, kstart=kstart)
         a = self._linear(f"{i}.o", o, self._w(p + "self_attn.o_proj.weight"), self._g(p + "self_attn.o_proj.weight"))
         q_gu = self._q8(f"{i}.gu")
         y, h = ops.add_rmsnorm(h, a, self._m(p + "post_attention_layernorm.weight"),
@@ -203,9 +203,11 @@ class LlamaForCausalLM:
                          self._g(p + "mlp.down_proj.weight"), q_down.out if q_down is not None else None)
         return m, h
 
-    def hidden_states(self, input_ids: torch.Tensor) -> torch.Tensor:
-        """Final-normed hidden states [B*T, d] in the compute dtype."""
+    def hidden_states(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Final-normed hidden states [B*T, d] in the compute dtype.  ``attention_mask`` (HF [B, T],
+        left or right padded) becomes a per-sequence key start for the attention kernels."""
         c = self.config
+        kstart = ops.key_start(attention_mask) if attention_mask is not None else None
         B, T = input_ids.shape
         cdt = self.compute_dtype
         eps = c.rms_norm_eps
@@ -227,9 +229,9 @@ class LlamaForCausalLM:
             nxt = f"model.layers.{i + 1}.input_layernorm.weight" if i + 1 < L else "model.norm.weight"
             if self.activation_checkpointing and self.training and torch.is_grad_enabled():
                 from torch.utils.checkpoint import checkpoint
-                m, h = checkpoint(self._layer, i, h, y, cos, sin, B, T, nxt, None, use_reentrant=False)
+                m, h = checkpoint(self._layer, i, h, y, cos, sin, B, T, nxt, None, kstart, use_reentrant=False)
             else:
-                m, h = self._layer(i, h, y, cos, sin, B, T, nxt, y8)
+                m, h = self._layer(i, h, y, cos, sin, B, T, nxt, y8, kstart)
             if hook is not None and i + 1 < L:
                 # layer i+1's gradients are final once the backward of the add+norm that produces its
                 # input (and owns its input_layernorm weight) has run: hook that norm's input
@@ -243,9 +245,10 @@ class LlamaForCausalLM:
     def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None, attention_mask=None,
                 loss_scale: float = 1.0, return_logits: bool = False, targets: Optional[torch.Tensor] = None
                 ) -> CausalLMOutput:
-        """``labels`` follow HF semantics (shifted internally, -100 ignored); ``attention_mask`` is
-        accepted for API parity: padded positions must be given label -100 by the caller."""
-        y = self.hidden_states(input_ids)
+        """``labels`` follow HF semantics (shifted internally, -100 ignored).  ``attention_mask``
+        follows HF too: pad keys are masked for every real token (left or right padding; pad positions
+        should carry label -100, as the HF data path sets them)."""
+        y = self.hidden_states(input_ids, attention_mask)
         lm = "lm_head.weight" if not self.config.tie_word_embeddings else "model.embed_tokens.weight"
         out = CausalLMOutput()
         if labels is not None or targets is not None:

@@ -6,7 +6,7 @@ from .linear import linear, wgrad_accumulate, set_wgrad_overlap, wgrad_overlap_e
 from .norm import rmsnorm, rmsnorm_res, add_rmsnorm
 from .embedding import embedding
 from .swiglu import swiglu
-from .attention import attention, rope_cache, set_attn_fused_stats
+from .attention import attention, rope_cache, set_attn_fused_stats, key_start, check_padding
 from .cross_entropy import lm_head_ce, IGNORE_INDEX
 from .optim import adamw_step, global_grad_norm, pseudograd, outer_nesterov
 from . import reference

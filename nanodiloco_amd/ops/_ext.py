@@ -137,6 +137,9 @@ def _declare(L: ctypes.CDLL):
         "nd_rope_inplace": [P, I, P, P, L64, I, I, I, I, I, I, P],
         # attention
         "nd_attn_fwd": [P, P, P, P, P, I, I, I, I, I, L64, L64, P, P, F, P],
+        "nd_attn_fwd_ks": [P, P, P, P, P, I, I, I, I, I, L64, L64, P, P, F, P, P],
+        "nd_attn_bwd_ks": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, L64, L64, P, P, F, I, P, P],
+        "nd_attn_bwd_fused_ks": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, L64, L64, P, P, F, I, P, P],
         "nd_attn_bwd_pre": [P, P, P, I, I, I, L64, L64, P],
         "nd_attn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, L64, L64, P, P, F, I, P],
         "nd_attn_bwd_fused": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, L64, L64, P, P, F, I, P],

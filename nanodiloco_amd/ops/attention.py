@@ -59,7 +59,7 @@ class FlashAttnFn(torch.autograd.Function):
     their store epilogues (rope_mode 2), so the gradient returned is w.r.t. the raw projection."""
 
     @staticmethod
-    def forward(ctx, qkv, cos, sin, B, T, nh, nkv, hd):
+    def forward(ctx, qkv, cos, sin, B, T, nh, nkv, hd, kstart=None):
         ld = qkv.shape[1]
         _rope(qkv, cos, sin, B, T, nh, nkv, hd, inverse=False)
         k = qkv[:, nh * hd:]
@@ -67,10 +67,12 @@ class FlashAttnFn(torch.autograd.Function):
         o = torch.empty(B * T, nh * hd, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(B, nh, T, dtype=torch.float32, device=qkv.device)
         L = _ext.lib()
-        _ext.check(L.nd_attn_fwd(_ext.ptr(qkv), _ext.ptr(k), _ext.ptr(v), _ext.ptr(o), _ext.ptr(lse),
-                                 B, nh, nkv, T, hd, ld, nh * hd, 0, 0, float(hd ** -0.5),
-                                 _ext.stream_ptr(qkv.device)), "nd_attn_fwd")
+        ks = _ext.ptr(kstart) if kstart is not None else 0
+        _ext.check(L.nd_attn_fwd_ks(_ext.ptr(qkv), _ext.ptr(k), _ext.ptr(v), _ext.ptr(o), _ext.ptr(lse),
+                                    B, nh, nkv, T, hd, ld, nh * hd, 0, 0, float(hd ** -0.5), ks,
+                                    _ext.stream_ptr(qkv.device)), "nd_attn_fwd_ks")
         ctx.save_for_backward(qkv, o, lse, cos, sin)
+        ctx.kstart = kstart
         ctx.dims = (B, T, nh, nkv, hd)
         return o
 
@@ -82,17 +84,18 @@ class FlashAttnFn(torch.autograd.Function):
         ld = qkv.shape[1]
         L = _ext.lib()
         dev = do.device
+        ks = _ext.ptr(ctx.kstart) if ctx.kstart is not None else 0
         if _FUSED_STATS["enabled"] and T % 64 == 0:
             # dQ kernel computes delta = rowsum(dO * O) itself and seeds the dK/dV kernel
             dqkv = torch.empty_like(qkv)
             k, v = qkv[:, nh * hd:], qkv[:, (nh + nkv) * hd:]
             dk, dv = dqkv[:, nh * hd:], dqkv[:, (nh + nkv) * hd:]
             ws = torch.empty(2, B, nh, T, dtype=torch.float32, device=dev)
-            _ext.check(L.nd_attn_bwd_fused(_ext.ptr(qkv), _ext.ptr(k), _ext.ptr(v), _ext.ptr(o), _ext.ptr(do),
-                                           _ext.ptr(lse), _ext.ptr(dqkv), _ext.ptr(dk), _ext.ptr(dv), _ext.ptr(ws),
-                                           B, nh, nkv, T, hd, ld, nh * hd, _ext.ptr(cos), _ext.ptr(sin),
-                                           float(hd ** -0.5), 2, _ext.stream_ptr(dev)), "nd_attn_bwd_fused")
-            return dqkv, None, None, None, None, None, None, None
+            _ext.check(L.nd_attn_bwd_fused_ks(_ext.ptr(qkv), _ext.ptr(k), _ext.ptr(v), _ext.ptr(o), _ext.ptr(do),
+                                              _ext.ptr(lse), _ext.ptr(dqkv), _ext.ptr(dk), _ext.ptr(dv), _ext.ptr(ws),
+                                              B, nh, nkv, T, hd, ld, nh * hd, _ext.ptr(cos), _ext.ptr(sin),
+                                              float(hd ** -0.5), 2, ks, _ext.stream_ptr(dev)), "nd_attn_bwd_fused_ks")
+            return dqkv, None, None, None, None, None, None, None, None
         delta = torch.empty(B, nh, T, dtype=torch.float32, device=dev)
         _ext.check(L.nd_attn_bwd_pre(_ext.ptr(o), _ext.ptr(do), _ext.ptr(delta), B, nh, T, hd, nh * hd,
                                      _ext.stream_ptr(dev)), "nd_attn_bwd_pre")
@@ -100,22 +103,44 @@ class FlashAttnFn(torch.autograd.Function):
         k, v = qkv[:, nh * hd:], qkv[:, (nh + nkv) * hd:]
         dk, dv = dqkv[:, nh * hd:], dqkv[:, (nh + nkv) * hd:]
         ws = torch.empty(2, B, nh, T, dtype=torch.float32, device=dev)  # -LSE/c, -delta for the dK/dV kernel
-        _ext.check(L.nd_attn_bwd(_ext.ptr(qkv), _ext.ptr(k), _ext.ptr(v), _ext.ptr(do), _ext.ptr(lse), _ext.ptr(delta),
-                                 _ext.ptr(dqkv), _ext.ptr(dk), _ext.ptr(dv), _ext.ptr(ws),
-                                 B, nh, nkv, T, hd, ld, nh * hd, _ext.ptr(cos), _ext.ptr(sin), float(hd ** -0.5), 2,
-                                 _ext.stream_ptr(dev)), "nd_attn_bwd")
-        return dqkv, None, None, None, None, None, None, None
+        _ext.check(L.nd_attn_bwd_ks(_ext.ptr(qkv), _ext.ptr(k), _ext.ptr(v), _ext.ptr(do), _ext.ptr(lse),
+                                    _ext.ptr(delta), _ext.ptr(dqkv), _ext.ptr(dk), _ext.ptr(dv), _ext.ptr(ws),
+                                    B, nh, nkv, T, hd, ld, nh * hd, _ext.ptr(cos), _ext.ptr(sin), float(hd ** -0.5), 2,
+                                    ks, _ext.stream_ptr(dev)), "nd_attn_bwd_ks")
+        return dqkv, None, None, None, None, None, None, None, None
+
+
+def key_start(attention_mask: torch.Tensor) -> torch.Tensor:
+    """Per-sequence first real key (int32 [B]) of an HF ``attention_mask`` [B, T] (1 = token, 0 = pad).
+
+    Left padding ([0..0, 1..1]) gives the pad count; right padding ([1..1, 0..0]) gives 0 -- causal
+    attention already keeps every real query off the trailing pad keys.  Masks with holes (a pad
+    between real tokens) are not expressible as a key start: ``check_padding`` rejects them."""
+    m = attention_mask.to(torch.int32)
+    return (m.cumsum(1) == 0).sum(1).to(torch.int32)
+
+
+def check_padding(attention_mask: torch.Tensor) -> None:
+    """Raise unless every row is left- or right-padded (one contiguous run of real tokens)."""
+    m = attention_mask.to(torch.int32)
+    transitions = (m[:, 1:] != m[:, :-1]).sum(1)
+    if bool((transitions > 2).any()) or bool(((transitions == 2) & (m[:, 0] == 1)).any()):
+        raise ValueError("attention_mask rows must be one contiguous run of tokens (left or right padding)")
 
 
 def attention(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, B: int, T: int, nh: int, nkv: int,
-              hd: int, inplace: bool = False) -> torch.Tensor:
+              hd: int, inplace: bool = False, kstart: torch.Tensor = None) -> torch.Tensor:
     """Causal self-attention with RoPE; qkv [B*T, (nh+2nkv)*hd] -> [B*T, nh*hd].
 
-    ``inplace=True`` lets the HIP path rotate q|k inside ``qkv`` itself (the model passes it for the
-    projection output it owns); otherwise a private copy is rotated."""
+    ``kstart`` (int32 [B], from :func:`key_start`) masks left padding: real queries (t >= kstart[b])
+    never see the pad keys t' < kstart[b] -- the reference's causal + padding mask
+    (REF/nanodiloco/main.py:79-88,109 -> HF SDPA).  ``inplace=True`` lets the HIP path rotate q|k
+    inside ``qkv`` itself (the model passes it for the projection output it owns); otherwise a private
+    copy is rotated."""
     if _ext.use_hip(qkv):
         x = qkv.contiguous()
         if not inplace and x.data_ptr() == qkv.data_ptr():
             x = x.clone()  # never rotate a caller-visible tensor
-        return FlashAttnFn.apply(x, cos, sin, B, T, nh, nkv, hd)
-    return ref.attention_block(qkv, cos, sin, B, T, nh, nkv, hd, use_sdpa=True)
+        ks = kstart.to(device=qkv.device, dtype=torch.int32).contiguous() if kstart is not None else None
+        return FlashAttnFn.apply(x, cos, sin, B, T, nh, nkv, hd, ks)
+    return ref.attention_block(qkv, cos, sin, B, T, nh, nkv, hd, use_sdpa=True, kstart=kstart)

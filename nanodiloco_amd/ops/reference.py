@@ -114,12 +114,29 @@ def causal_attention(q, k, v, scale: Optional[float] = None):
     return torch.matmul(p, v.float()).to(q.dtype)
 
 
+def padded_causal_mask(kstart: torch.Tensor, T: int) -> torch.Tensor:
+    """Boolean [B, 1, T, T] (True = attend): causal & key is not a left pad (HF's sdpa mask).  Pad
+    query rows are fully masked; torch SDPA returns 0 for them, as the attention kernels do."""
+    t = torch.arange(T, device=kstart.device)
+    causal = t[None, :] <= t[:, None]
+    real_k = t.view(1, 1, T) >= kstart.view(-1, 1, 1).to(t.dtype)
+    return (causal[None] & real_k).unsqueeze(1)
+
+
 def attention_block(qkv: torch.Tensor, cos, sin, B: int, T: int, nh: int, nkv: int, hd: int,
-                    use_sdpa: bool = True) -> torch.Tensor:
-    """qkv [B*T, (nh+2nkv)*hd] -> RoPE -> causal attention -> [B*T, nh*hd] (autograd-capable)."""
+                    use_sdpa: bool = True, kstart: torch.Tensor = None) -> torch.Tensor:
+    """qkv [B*T, (nh+2nkv)*hd] -> RoPE -> causal attention -> [B*T, nh*hd] (autograd-capable).
+    ``kstart``: left-padding key start per sequence (see ``ops.attention.key_start``)."""
     q, k, v = split_qkv(qkv, B, T, nh, nkv, hd)
     q = apply_rope(q, cos[:T], sin[:T])
     k = apply_rope(k, cos[:T], sin[:T])
+    if kstart is not None:
+        mask = padded_causal_mask(kstart.to(qkv.device), T)
+        if nkv != nh:
+            k = k.repeat_interleave(nh // nkv, dim=1)
+            v = v.repeat_interleave(nh // nkv, dim=1)
+        o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask)
+        return o.transpose(1, 2).reshape(B * T, nh * hd)
     if use_sdpa:
         o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=(nkv != nh))
     else:

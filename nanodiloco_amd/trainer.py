@@ -187,10 +187,12 @@ class Trainer:
                 batch = next(self.data)
                 if micro == self.grad_accum - 1:
                     self.inner_sync.arm()
-                if self.graphed is not None:
+                mask = batch.get("attention_mask")  # HF path: padded batches (reference main.py:79-88,109)
+                if self.graphed is not None and mask is None:
                     l = self.graphed(batch["input_ids"], batch["labels"], self.loss_scale).clone()
                 else:
-                    out = self.model(batch["input_ids"], labels=batch["labels"], loss_scale=self.loss_scale)
+                    out = self.model(batch["input_ids"], labels=batch["labels"], attention_mask=mask,
+                                     loss_scale=self.loss_scale)
                     out.loss.backward()
                     l = out.loss.detach()
                 loss_sum = l if loss_sum is None else loss_sum + l

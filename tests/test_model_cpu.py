@@ -107,3 +107,51 @@ def test_rmsnorm_res_fuses_residual_grad():
     xr = x.clone().requires_grad_(True)
     (ops.rmsnorm(xr, w, None, 1e-5) * up).sum().backward()
     torch.testing.assert_close(xx.grad, xr.grad)
+
+
+@pytest.mark.parametrize("side", ["left", "right"])
+def test_padded_batch_matches_hf_attention_mask(side):
+    """Padded batches (the reference's tokenizer.pad + attention_mask, REF/nanodiloco/main.py:79-88,109):
+    loss, grads and the logits of every real token match HF given the same attention_mask."""
+    torch.manual_seed(0)
+    cfgd = dict(hidden_size=64, intermediate_size=96, num_attention_heads=4, num_key_value_heads=2,
+                num_hidden_layers=2, vocab_size=101, rms_norm_eps=1e-5)
+    c = LlamaConfig.from_dict(cfgd)
+    m = LlamaForCausalLM(c).init_weights(3)
+    # the reference builds LlamaForCausalLM with the default (sdpa) attention: fully masked (left-pad)
+    # query rows come out as 0, which decides the prediction made at the last pad position
+    hf = transformers.LlamaForCausalLM(transformers.LlamaConfig(**cfgd, attn_implementation="sdpa")).float()
+    hf.load_state_dict({k: v.clone() for k, v in m.state_dict().items()}, strict=False)
+    B, T = 3, 20
+    ids = torch.randint(0, c.vocab_size, (B, T))
+    mask = torch.ones(B, T, dtype=torch.long)
+    for b, npad in enumerate([0, 5, 11]):
+        if npad:
+            if side == "left":
+                mask[b, :npad] = 0
+            else:
+                mask[b, T - npad:] = 0
+    ids[mask == 0] = 2  # pad token
+    labels = ids.clone()
+    labels[mask == 0] = -100
+    out = m(ids, labels=labels, attention_mask=mask)
+    out.loss.backward()
+    ho = hf(input_ids=ids, attention_mask=mask, labels=labels)
+    ho.loss.backward()
+    assert abs(out.loss.item() - ho.loss.item()) < 1e-5, (out.loss.item(), ho.loss.item())
+    for n, p in hf.named_parameters():
+        assert torch.allclose(p.grad, m.store.grad_view(n), atol=2e-6, rtol=1e-4), n
+    logits = m(ids, attention_mask=mask).logits
+    # left: every position matches (pad rows attend to nothing on both sides); right: trailing pad
+    # queries still see the real keys in HF (and everything causal here) -- they carry no loss
+    sel = torch.ones_like(mask, dtype=torch.bool) if side == "left" else mask.bool()
+    assert torch.allclose(logits[sel], ho.logits[sel], atol=1e-5)
+
+
+def test_key_start_and_padding_check():
+    from nanodiloco_amd.ops import check_padding, key_start
+    mask = torch.tensor([[0, 0, 1, 1], [1, 1, 1, 0], [1, 1, 1, 1], [0, 1, 1, 1]])
+    assert key_start(mask).tolist() == [2, 0, 0, 1]
+    check_padding(mask)
+    with pytest.raises(ValueError):
+        check_padding(torch.tensor([[1, 0, 1, 1]]))
