@@ -4,7 +4,8 @@
 // (16-B loads, CH chunks of 8 per thread: V=32000 -> 16 chunks = 64 VGPRs of packed bf16), so the
 // row is read from HBM exactly once and written once:
 //   m = max(x), s = sum exp(x - m), lse = m + log s            (fp32, block reductions)
-//   loss_row = lse - x[target]            -> block sum -> one atomicAdd into loss_sum
+//   loss_row = lse - x[target]            -> block sum -> one atomicAdd into loss_sum (or, with
+//                                           row_loss != nullptr, one store per row: deterministic)
 //   x <- (exp(x - lse) - [j == target]) * scale               (dlogits, compute dtype)
 // scale = loss_scale / n_valid lives in device memory (no host sync).  Rows whose target is
 // ignore_index contribute 0 loss and 0 gradient.  Larger vocabularies use the two-pass variant.
@@ -29,7 +30,8 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 template <int DT, int CH>
 __global__ void __launch_bounds__(256) ce_reg_kernel(void* __restrict__ logits, const int64_t* __restrict__ targets,
                                                      float* __restrict__ loss_sum, const float* __restrict__ scale_p,
-                                                     int V, int ignore, float* __restrict__ lse_out) {
+                                                     int V, int ignore, float* __restrict__ lse_out,
+                                                     float* __restrict__ row_loss) {
   __shared__ float red[8];
   const int64_t row = blockIdx.x;
   const int64_t base = row * (int64_t)V;
@@ -80,7 +82,10 @@ __global__ void __launch_bounds__(256) ce_reg_kernel(void* __restrict__ logits, 
   }
   __syncthreads();
   picked = block_sum<256>(picked, red);
-  if (threadIdx.x == 0 && valid) atomicAdd(loss_sum, lse - picked);
+  if (threadIdx.x == 0) {
+    if (row_loss) row_loss[row] = valid ? lse - picked : 0.f;  // deterministic mode: summed in order later
+    else if (valid) atomicAdd(loss_sum, lse - picked);
+  }
 }
 
 
@@ -91,7 +96,8 @@ __global__ void __launch_bounds__(256) ce_reg_kernel(void* __restrict__ logits, 
 template <int CH>
 __global__ void __launch_bounds__(256) ce_bf16_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
                                                       float* __restrict__ loss_sum, const float* __restrict__ scale_p,
-                                                      int V, int ignore, float* __restrict__ lse_out) {
+                                                      int V, int ignore, float* __restrict__ lse_out,
+                                                     float* __restrict__ row_loss) {
   constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
   __shared__ float red[8];
   const int64_t row = blockIdx.x;
@@ -162,14 +168,18 @@ __global__ void __launch_bounds__(256) ce_bf16_kernel(bf16_t* __restrict__ logit
   if (threadIdx.x == 0 && lse_out) lse_out[row] = lse;
   __syncthreads();
   picked = block_sum<256>(picked, red);
-  if (threadIdx.x == 0 && valid) atomicAdd(loss_sum, lse - picked);
+  if (threadIdx.x == 0) {
+    if (row_loss) row_loss[row] = valid ? lse - picked : 0.f;  // deterministic mode: summed in order later
+    else if (valid) atomicAdd(loss_sum, lse - picked);
+  }
 }
 
 // Generic two-pass variant (any V, scalar accesses): online max/sum, then gradient write.
 template <int DT>
 __global__ void __launch_bounds__(256) ce_generic_kernel(void* __restrict__ logits, const int64_t* __restrict__ targets,
                                                          float* __restrict__ loss_sum, const float* __restrict__ scale_p,
-                                                         int V, int ignore, float* __restrict__ lse_out) {
+                                                         int V, int ignore, float* __restrict__ lse_out,
+                                                     float* __restrict__ row_loss) {
   __shared__ float red[8];
   const int64_t row = blockIdx.x;
   const int64_t base = row * (int64_t)V;
@@ -204,28 +214,31 @@ __global__ void __launch_bounds__(256) ce_generic_kernel(void* __restrict__ logi
   if (threadIdx.x == 0 && lse_out) lse_out[row] = lse;
   __syncthreads();
   picked = block_sum<256>(picked, red);
-  if (threadIdx.x == 0 && valid) atomicAdd(loss_sum, lse - picked);
+  if (threadIdx.x == 0) {
+    if (row_loss) row_loss[row] = valid ? lse - picked : 0.f;  // deterministic mode: summed in order later
+    else if (valid) atomicAdd(loss_sum, lse - picked);
+  }
 }
 
 ND_API int nd_ce_fwd_bwd(void* logits, int dt, const int64_t* targets, float* loss_sum, const float* scale,
-                         int64_t n, int V, int ignore, float* lse_out, void* /*reserved*/, float /*reserved*/,
+                         int64_t n, int V, int ignore, float* lse_out, float* row_loss, float /*reserved*/,
                          hipStream_t s) {
   if (n <= 0) return 0;
   dim3 g((unsigned)n), b(256);
   if (V % 8 == 0 && V <= 256 * 8 * 16) {
     if (V <= 256 * 8 * 4) {
-      if (dt == BF16) hipLaunchKernelGGL((ce_reg_kernel<BF16, 4>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out);
-      else hipLaunchKernelGGL((ce_reg_kernel<F32, 4>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out);
+      if (dt == BF16) hipLaunchKernelGGL((ce_reg_kernel<BF16, 4>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
+      else hipLaunchKernelGGL((ce_reg_kernel<F32, 4>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
     } else {
       const char* ev = getenv("ND_CE");
       if (dt == BF16 && !(ev && ev[0] == 'r'))
-        hipLaunchKernelGGL((ce_bf16_kernel<16>), g, b, 0, s, (bf16_t*)logits, targets, loss_sum, scale, V, ignore, lse_out);
-      else if (dt == BF16) hipLaunchKernelGGL((ce_reg_kernel<BF16, 16>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out);
-      else hipLaunchKernelGGL((ce_reg_kernel<F32, 16>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out);
+        hipLaunchKernelGGL((ce_bf16_kernel<16>), g, b, 0, s, (bf16_t*)logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
+      else if (dt == BF16) hipLaunchKernelGGL((ce_reg_kernel<BF16, 16>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
+      else hipLaunchKernelGGL((ce_reg_kernel<F32, 16>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
     }
   } else {
-    if (dt == BF16) hipLaunchKernelGGL(ce_generic_kernel<BF16>, g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out);
-    else hipLaunchKernelGGL(ce_generic_kernel<F32>, g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out);
+    if (dt == BF16) hipLaunchKernelGGL(ce_generic_kernel<BF16>, g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
+    else hipLaunchKernelGGL(ce_generic_kernel<F32>, g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
   }
   ND_LAUNCH_CHECK();
 }

@@ -72,10 +72,8 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const void* __restrict
                                                           void* __restrict__ da, float* __restrict__ part,
                                                           int64_t rows, int cols, Fp8Out q8) {
   float qmax = 0.f;
-  extern __shared__ __attribute__((aligned(16))) float sdw[];
+  extern __shared__ __attribute__((aligned(16))) float sdw[];  // [4 waves][cols] weight-gradient partials
   const int lane = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < cols; i += 256) sdw[i] = 0.f;
-  __syncthreads();
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   float dwacc[NCH][8];
@@ -133,15 +131,17 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const void* __restrict
     }
   }
   if (Q) block_amax_commit<256>(qmax, q8.amax, q8.parts);
+  // each wave stores its partial row; the block's four are summed in wave order (no LDS float
+  // atomics: their arrival order made the weight gradient non-reproducible in the last bits)
+  float* mine = sdw + (threadIdx.x >> 6) * cols;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = (c * 64 + lane) * 8;
-    if (col < cols)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) atomicAdd(&sdw[col + j], dwacc[c][j]);
+    if (col < cols) Vec8<F32>::store(mine, col, dwacc[c]);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < cols; i += 256) part[(int64_t)blockIdx.x * cols + i] = sdw[i];
+  for (int i = threadIdx.x; i < cols; i += 256)
+    part[(int64_t)blockIdx.x * cols + i] = ((sdw[i] + sdw[cols + i]) + sdw[2 * cols + i]) + sdw[3 * cols + i];
 }
 
 // ------------------------------------------------------------------------------------ launchers
@@ -197,7 +197,7 @@ static int bwd_dispatch(const void* dy, int dydt, const float* h, const float* w
   int64_t blocks = (rows + 63) / 64;
   if (blocks > 1024) blocks = 1024;
   dim3 g((unsigned)blocks), b(256);
-  size_t lds = (size_t)cols * sizeof(float);
+  size_t lds = 4 * (size_t)cols * sizeof(float);
   const Fp8Out none{nullptr, nullptr, nullptr, 1, 0};
   if (q8) {  // fused fp8 side output: bf16 dy and da only
     if (dydt != BF16 || dadt != BF16 || da == nullptr) return (int)hipErrorInvalidValue;

@@ -9,6 +9,7 @@ from .swiglu import swiglu
 from .attention import attention, rope_cache, set_attn_fused_stats, key_start, check_padding
 from .cross_entropy import lm_head_ce, IGNORE_INDEX
 from .optim import adamw_step, global_grad_norm, pseudograd, outer_nesterov
+from .determinism import set_deterministic, deterministic
 from . import reference
 
 __all__ = ["hip_available", "set_backend", "get_backend", "ExtensionMissing", "linear", "wgrad_accumulate",

@@ -25,6 +25,7 @@ from __future__ import annotations
 import torch
 
 from . import _ext
+from .determinism import deterministic
 from .linear import library_gemm_fence, wgrad_accumulate
 
 IGNORE_INDEX = -100
@@ -46,6 +47,7 @@ class LMHeadCEFn(torch.autograd.Function):
         dy = torch.empty_like(y)
         loss_sum = torch.zeros(1, dtype=torch.float32, device=y.device)
         hip = _ext.use_hip(y)
+        det = deterministic()
         chunk = chunk_rows or _chunk_rows(V, y.element_size() if hip else 4)
         if not chunk_rows and n > chunk:  # equal-sized chunks: one GEMM shape, one tuned kernel
             nch = -(-n // chunk)
@@ -56,9 +58,13 @@ class LMHeadCEFn(torch.autograd.Function):
             if hip:
                 library_gemm_fence(y.device)
                 logits = torch.mm(yc, w.t())
+                rows = torch.empty(e - s, dtype=torch.float32, device=y.device) if det else None
                 _ext.check(_ext.lib().nd_ce_fwd_bwd(_ext.ptr(logits), _ext.dtcode(logits), _ext.ptr(tc),
                                                     _ext.ptr(loss_sum), _ext.ptr(scale), e - s, V, IGNORE_INDEX,
-                                                    0, 0, 0.0, _ext.stream_ptr(y.device)), "nd_ce_fwd_bwd")
+                                                    0, _ext.ptr(rows) if det else 0, 0.0,
+                                                    _ext.stream_ptr(y.device)), "nd_ce_fwd_bwd")
+                if det:  # per-row losses, one ordered reduction (no float atomics)
+                    loss_sum += rows.sum()
                 dl = logits
             else:
                 logits = torch.mm(yc.float(), w.float().t())

@@ -3,13 +3,15 @@ backward scatter-adds the residual gradient rows into the flat fp32 grad buffer.
 
 HIP path: ``nd_embedding_fwd`` (one wave per token row, 16-B vector loads) and
 ``nd_embedding_bwd`` (one wave per token row, f32 atomics on whole contiguous rows -- the
-access shape the MI355X atomic unit serves at full rate, MI355X_MICROARCH.md §Global float atomics).
+access shape the MI355X atomic unit serves at full rate, MI355X_MICROARCH.md §Global float atomics),
+or, in deterministic mode (ops/determinism.py), ``nd_embedding_bwd_sorted`` over a stable argsort.
 """
 from __future__ import annotations
 
 import torch
 
 from . import _ext
+from .determinism import deterministic
 
 
 class EmbeddingFn(torch.autograd.Function):
@@ -36,8 +38,15 @@ class EmbeddingFn(torch.autograd.Function):
             dy = dy.contiguous()
             if ctx.hip:
                 n, d = dy.shape
-                _ext.check(_ext.lib().nd_embedding_bwd(_ext.ptr(ids), _ext.ptr(dy), _ext.ptr(ctx.gw), n, d, ctx.vocab,
-                                                       _ext.stream_ptr(dy.device)), "nd_embedding_bwd")
+                if deterministic():
+                    perm = torch.argsort(ids, stable=True)
+                    sid = ids.index_select(0, perm).contiguous()
+                    _ext.check(_ext.lib().nd_embedding_bwd_sorted(_ext.ptr(sid), _ext.ptr(perm), _ext.ptr(dy),
+                                                                  _ext.ptr(ctx.gw), n, d, ctx.vocab,
+                                                                  _ext.stream_ptr(dy.device)), "nd_embedding_bwd_sorted")
+                else:
+                    _ext.check(_ext.lib().nd_embedding_bwd(_ext.ptr(ids), _ext.ptr(dy), _ext.ptr(ctx.gw), n, d,
+                                                           ctx.vocab, _ext.stream_ptr(dy.device)), "nd_embedding_bwd")
             else:
                 ctx.gw.index_add_(0, ids, dy.float())
         # the embedding backward is the last op of the model's backward: join the side-stream

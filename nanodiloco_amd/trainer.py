@@ -81,6 +81,7 @@ class TrainArgs:
     tokenizer: str = "huggyllama/llama-7b"
     debug_checks: bool = False
     mask_pad_labels: bool = True
+    deterministic: bool = False    # bitwise-reproducible step: no float atomics (ops/determinism.py)
     skip_nonfinite: bool = False   # device-side skip of inner steps whose grad norm is NaN/Inf (no host sync)
     collective_timeout_s: float = 1800.0
     phase_timing: bool = True      # HIP-event timing of fwd+bwd / inner optimizer / outer step (logged)
@@ -116,6 +117,7 @@ class Trainer:
             raise ValueError("total_steps must be a multiple of inner_steps")  # REF main.py:69
         ops.set_backend(a.ops)
         ops.set_wgrad_overlap(a.wgrad_overlap)
+        ops.set_deterministic(a.deterministic)
         self.env = env or init_distributed(a.backend, a.inner_dp, device=None if a.device == "auto" else a.device,
                                            timeout_s=a.collective_timeout_s)
         e = self.env
