@@ -321,7 +321,7 @@ struct TileDma {
 };
 
 // =============================================================================== forward
-template <int HD, bool ROPE, bool DMA = false>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
+template <int HD, bool ROPE, bool DMA = false, bool PAD = false>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int nh, int nkv, int T,
@@ -336,7 +336,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
   const int qb = nqb - 1 - (int)(blockIdx.x / bh_count);  // longest causal rows first
   const int bh = blockIdx.x % bh_count;
   const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
-  const int ks = KS ? KS[b] : 0;  // left padding: keys < ks are masked for the real queries (>= ks)
+  const int ks = PAD ? KS[b] : 0;  // PAD (left-padded batch): keys < ks are masked for every query
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15;
   const int q0w = qb * 128 + w * 32, qi = q0w + c32;
@@ -404,13 +404,13 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
 #pragma unroll
         for (int t = 0; t < NT; ++t) s[kt] = mfma32(ka[kt][t], qf[t], s[kt]);
       }
-      if ((k0 + BN - 1 > q0w) || (k0 + BN > T) || (k0 < ks)) {
+      if ((k0 + BN - 1 > q0w) || (k0 + BN > T) || (PAD && k0 < ks)) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (key > qi || key >= T || key < ks) s[kt][r] = -INFINITY;
+            if (key > qi || key >= T || (PAD && key < ks)) s[kt][r] = -INFINITY;
           }
       }
       float mx = -INFINITY;
@@ -421,7 +421,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
       mx = pair_max32(mx) * c;  // raw-score max -> log2 domain (c > 0)
       const float mnew = fmaxf(m, mx);
       // a row with no visible key yet (a left-pad query: every key masked) keeps p = 0, l = 0
-      const float mref = mnew == -INFINITY ? 0.f : mnew;
+      const float mref = (PAD && mnew == -INFINITY) ? 0.f : mnew;
       const float alpha = fexp2(m - mref);
       m = mnew;
       float rs = 0.f;
@@ -503,7 +503,7 @@ __global__ void __launch_bounds__(256) attn_bwd_pre_kernel(const bf16_t* __restr
 // attn_neg_stats_kernel: each lane already holds half of its query's dO row, so it loads the same
 // half of O, dots, and one lane^32 exchange gives delta = rowsum(dO * O); the kernel then writes
 // -delta and -LSE/c (the seeds of the dK/dV kernel, which therefore runs after this one).
-template <int HD, bool ROPE, bool ROPE_OUT, bool DMA = false, bool PRE = false>  // DMA: LDS-DMA K/V staging
+template <int HD, bool ROPE, bool ROPE_OUT, bool DMA = false, bool PRE = false, bool PAD = false>  // DMA: LDS-DMA K/V staging
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                              const bf16_t* __restrict__ V, const bf16_t* __restrict__ dO,
                                                              const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -522,7 +522,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
   const int qb = nqb - 1 - (int)(blockIdx.x / bh_count);
   const int bh = blockIdx.x % bh_count;
   const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
-  const int ks = KS ? KS[b] : 0;
+  const int ks = PAD ? KS[b] : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15;
   const int q0w = qb * 128 + w * 32, qi = q0w + c32;
@@ -599,7 +599,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
       if (j + 1 < ntiles) dma_issue(j + 1);
     }
     if (k0 <= q0w + 31) {
-      const bool diag = (k0 + BN - 1 > q0w) || (k0 + BN > T) || (qi >= T) || (k0 < ks);
+      const bool diag = (k0 + BN - 1 > q0w) || (k0 + BN > T) || (qi >= T) || (PAD && k0 < ks);
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         if (k0 + kt * 32 > q0w + 31) continue;  // this 32-key half is above the wave's diagonal
@@ -627,7 +627,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const float p = (key <= qi && key < T && qi < T && key >= ks) ? fexp2(fmaf(s[r], c, -lse)) : 0.f;
+            const float p = (key <= qi && key < T && qi < T && (!PAD || key >= ks)) ? fexp2(fmaf(s[r], c, -lse)) : 0.f;
             dp[r] = p * (dp[r] - dlt);
           }
         }
@@ -657,7 +657,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
 
 // dK, dV: per 128 keys of one (b, kv head); loops over the GQA group's query heads and 64-query
 // tiles from the diagonal to T.
-template <int HD, bool ROPE, bool ROPE_OUT>
+template <int HD, bool ROPE, bool ROPE_OUT, bool PAD = false>
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                                const bf16_t* __restrict__ V, const bf16_t* __restrict__ dO,
                                                                const float* __restrict__ LSE,
@@ -677,7 +677,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
   const int kb = (int)(blockIdx.x / bk_count);  // small kb = longest query range: dispatched first
   const int bk = blockIdx.x % bk_count;
   const int b = bk / nkv, kvh = bk % nkv;
-  const int ks = KS ? KS[b] : 0;
+  const int ks = PAD ? KS[b] : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15;
   const int kw0 = kb * 128 + w * 32, key = kw0 + c32;
@@ -769,7 +769,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
         s = mfma32(qa[t], kf[t], s);
         dp = mfma32(da[t], vf[t], dp);
       }
-      const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T) || (kw0 < ks);
+      const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T) || (PAD && kw0 < ks);
       if (!diag) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -781,7 +781,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qq = qsub + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float p = (key <= qq && qq < T && key < T && key >= ks) ? fexp2(s[r] * c) : 0.f;
+          const float p = (key <= qq && qq < T && key < T && (!PAD || key >= ks)) ? fexp2(s[r] * c) : 0.f;
           s[r] = p;
           dp[r] = p * dp[r];
         }
@@ -808,20 +808,20 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
 }
 
 // ------------------------------------------------------------------------------------ launchers
-template <int HD>
+template <int HD, bool PAD>
 static int fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, int B, int nh, int nkv, int T,
                       int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, const int* ks,
                       hipStream_t s) {
   const int nqb = (T + 127) / 128;
   const dim3 g(nqb * B * nh), b(256);
   if (cosT)
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, true>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, true, false, PAD>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   else if (T % 64 == 0 && !(getenv("ND_ATTN_FWD") && getenv("ND_ATTN_FWD")[0] == 'r'))
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, false, true>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k,
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, false, true, PAD>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k,
                        (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   else
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, false>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, false, false, PAD>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   ND_LAUNCH_CHECK();
 }
@@ -836,9 +836,13 @@ ND_API int nd_attn_fwd_ks(const void* q, const void* k, const void* v, void* o, 
                           const int* ks, hipStream_t s) {
   if (nh % nkv || (ld % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
   switch (hd) {
-    case 32: return fwd_launch<32>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
-    case 64: return fwd_launch<64>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
-    case 128: return fwd_launch<128>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
+#define ND_FW(H) \
+    case H: return ks ? fwd_launch<H, true>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s) \
+                      : fwd_launch<H, false>(q, k, v, o, lse, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
+    ND_FW(32)
+    ND_FW(64)
+    ND_FW(128)
+#undef ND_FW
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -879,7 +883,7 @@ __global__ void __launch_bounds__(256) attn_neg_stats_kernel(const float* __rest
   }
 }
 
-template <int HD, bool ROPE_OUT, int BQ = 64>
+template <int HD, bool ROPE_OUT, int BQ = 64, bool PAD = false>
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ NL, const float* __restrict__ ND, bf16_t* __restrict__ dK,
@@ -898,7 +902,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
   const int kb = (int)(blockIdx.x / bk_count);
   const int bk = blockIdx.x % bk_count;
   const int b = bk / nkv, kvh = bk % nkv;
-  const int ks = KS ? KS[b] : 0;
+  const int ks = PAD ? KS[b] : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15;
   const int kw0 = kb * 128 + w * 32, key = kw0 + c32;
@@ -996,7 +1000,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
         s = mfma32(qa[t], kf[t], s);
         dp = mfma32(da[t], vf[t], dp);
       }
-      const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T) || (kw0 < ks);
+      const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T) || (PAD && kw0 < ks);
       if (!diag) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -1008,7 +1012,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qq = qsub + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float p = (key <= qq && qq < T && key < T && key >= ks) ? fexp2(s[r] * c) : 0.f;
+          const float p = (key <= qq && qq < T && key < T && (!PAD || key >= ks)) ? fexp2(s[r] * c) : 0.f;
           s[r] = p;
           dp[r] = p * dp[r];
         }
@@ -1031,7 +1035,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
   }
 }
 
-template <int HD, bool ROPE, bool ROPE_OUT>
+template <int HD, bool ROPE, bool ROPE_OUT, bool PAD>
 static void bwd_launch_t(const void* q, const void* k, const void* v, const void* dout, const float* lse,
                          const float* delta, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T,
                          int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, const int* ks,
@@ -1046,24 +1050,24 @@ static void bwd_launch_t(const void* q, const void* k, const void* v, const void
                        1.f / (scale * LOG2E));
     const char* bq = getenv("ND_DKDV_BQ");  // "64": 64-query tiles (A/B); default 128 when T allows
     if (!(bq && bq[0] == '6') && T % 128 == 0)
-      hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128>), dim3(nb * B * nkv), dim3(256), 0, s,
+      hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                          (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
                          (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
     else
-      hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
+      hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 64, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                          (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
                          (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   } else {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, ROPE, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, ROPE, ROPE_OUT, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,
                        (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   }
   if (dma)
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT, !ROPE>), dim3(nb * B * nh), dim3(256), 0, s,
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT, !ROPE, false, PAD>), dim3(nb * B * nh), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,
                        (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, nullptr, nullptr, nullptr, ks);
   else
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT>), dim3(nb * B * nh), dim3(256), 0, s, (const bf16_t*)q,
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT, false, false, PAD>), dim3(nb * B * nh), dim3(256), 0, s, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, nh, nkv,
                        T, ld, ldo, scale, cosT, sinT, nullptr, nullptr, nullptr, ks);
 }
@@ -1075,11 +1079,11 @@ static int bwd_launch(const void* q, const void* k, const void* v, const void* d
                       void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo,
                       const float* cosT, const float* sinT, float scale, int rope_mode, const int* ks, hipStream_t s) {
   if (rope_mode == 1)
-    bwd_launch_t<HD, true, true>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
+    (ks ? bwd_launch_t<HD, true, true, true> : bwd_launch_t<HD, true, true, false>)(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
   else if (rope_mode == 2)
-    bwd_launch_t<HD, false, true>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
+    (ks ? bwd_launch_t<HD, false, true, true> : bwd_launch_t<HD, false, true, false>)(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
   else
-    bwd_launch_t<HD, false, false>(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
+    (ks ? bwd_launch_t<HD, false, false, true> : bwd_launch_t<HD, false, false, false>)(q, k, v, dout, lse, delta, dq, dk, dv, ws, B, nh, nkv, T, ld, ldo, cosT, sinT, scale, ks, s);
   ND_LAUNCH_CHECK();
 }
 
@@ -1109,7 +1113,7 @@ ND_API int nd_attn_bwd(const void* q, const void* k, const void* v, const void* 
 // Backward with the row statistics fused into the dQ kernel (PRE): dQ (writes -delta, -LSE/c into
 // ws) -> dK/dV; no attn_bwd_pre / attn_neg_stats passes.  LDS-DMA kernels only: q/k already rotated
 // (rope_mode 0 or 2), T % 64 == 0.  ws: 2 * B * nh * T floats.
-template <int HD, bool ROPE_OUT>
+template <int HD, bool ROPE_OUT, bool PAD>
 static int bwd_fused_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
                             const float* lse, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T,
                             int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, const int* ks,
@@ -1117,15 +1121,15 @@ static int bwd_fused_launch(const void* q, const void* k, const void* v, const v
   const int nb = (T + 127) / 128;
   const int64_t n = (int64_t)B * nh * T;
   float *nl = ws, *nd = ws + n;
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, ROPE_OUT, true, true>), dim3(nb * B * nh), dim3(256), 0, s,
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, ROPE_OUT, true, true, PAD>), dim3(nb * B * nh), dim3(256), 0, s,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
                      (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks);
   if (T % 128 == 0)
-    hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128>), dim3(nb * B * nkv), dim3(256), 0, s,
+    hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
                        (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   else
-    hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT>), dim3(nb * B * nkv), dim3(256), 0, s,
+    hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 64, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
                        (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
   ND_LAUNCH_CHECK();
@@ -1140,9 +1144,9 @@ ND_API int nd_attn_bwd_fused_ks(const void* q, const void* k, const void* v, con
   switch (hd) {
 #define ND_BF(H)                                                                                               \
   case H:                                                                                                      \
-    return rope_mode == 2 ? bwd_fused_launch<H, true>(q, k, v, o, dout, lse, dq, dk, dv, ws, B, nh, nkv, T, ld, \
+    return rope_mode == 2 ? (ks ? bwd_fused_launch<H, true, true> : bwd_fused_launch<H, true, false>)(q, k, v, o, dout, lse, dq, dk, dv, ws, B, nh, nkv, T, ld, \
                                                       ldo, cosT, sinT, scale, ks, s)                           \
-                          : bwd_fused_launch<H, false>(q, k, v, o, dout, lse, dq, dk, dv, ws, B, nh, nkv, T, ld, \
+                          : (ks ? bwd_fused_launch<H, false, true> : bwd_fused_launch<H, false, false>)(q, k, v, o, dout, lse, dq, dk, dv, ws, B, nh, nkv, T, ld, \
                                                        ldo, cosT, sinT, scale, ks, s);
     ND_BF(32)
     ND_BF(64)
