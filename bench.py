@@ -74,6 +74,8 @@ def parse():
                     help="attention backward: row statistics inside the dQ kernel (0: separate passes)")
     ap.add_argument("--dgrad-t", type=int, default=1, choices=[0, 1],
                     help="input-gradient GEMMs on transposed weight copies (K-contiguous NT layout)")
+    ap.add_argument("--fused-swiglu", type=int, default=0, choices=[0, 1],
+                    help="gate|up GEMM with SwiGLU in the own GEMM's epilogue (1) or hipBLASLt + swiglu kernel (0)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
     ap.add_argument("--fp8-wgrad", action="store_true", help="with --fp8: weight-gradient GEMM in fp8 too")
     ap.add_argument("--fp8-fused-quant", type=int, default=1, choices=[0, 1],
@@ -86,6 +88,7 @@ def main():
     a = parse()
     ops.set_backend(a.ops)
     ops.set_wgrad_overlap(a.wgrad_overlap)
+    ops.set_fused_swiglu(bool(a.fused_swiglu))
     ops.set_dgrad_transposed(bool(a.dgrad_t))
     ops.set_attn_fused_stats(bool(a.attn_fused_stats))
     if a.fp8:
@@ -228,6 +231,7 @@ def main():
             "final_loss": round(final_loss, 4),
             "tuned_gemm": enable_tuned_gemms(env.device) if env.device.type == "cuda" and not a.no_tuned_gemm else False,
             "wgrad_overlap": ops.wgrad_overlap_enabled(),
+            "fused_swiglu_gemm": ops.fused_swiglu_enabled(),
             "dgrad_transposed": ops.dgrad_transposed_enabled(),
             "ops": ops.get_backend() if a.ops != "auto" else ("hip" if env.device.type == "cuda" else "torch"),
         }

@@ -468,7 +468,7 @@ __global__ void __launch_bounds__(512, 2) gemm_nt_kernel(const bf16_t* __restric
 // PERSIST (variant 3): one workgroup per CU walks tiles first, first + G, ... (XCD-remapped so the
 // 32 workgroups of one XCD work on neighbouring tiles); the LDS-DMA stream runs ACROSS tile
 // boundaries, so the next tile's first K-tiles land while this tile's epilogue stores drain.
-template <int EPI, int HD, bool PERSIST, int SWZ, int ABL = 0, int LD = 0>
+template <int EPI, int HD, bool PERSIST, int SWZ, int ABL = 0, int LD = 0, int STP = 0>
 __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                        bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
                                                        int64_t ldb, int64_t ldc, Epi ep, int GM) {
@@ -732,7 +732,7 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict_
           const int row = i * 4 + q;  // 0..31 inside this pass
           const u32x4 d = *reinterpret_cast<const u32x4*>(cst + row * RS + (lane & 15) * 8);
           const int mr = wm * 128 + pass * 32 + row;
-          __builtin_amdgcn_raw_buffer_store_b128(d, crs, coff == 0x80000000u ? coff : coff + (uint32_t)(mr * ldc * 2), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(d, crs, coff == 0x80000000u ? coff : coff + (uint32_t)(mr * ldc * 2), 0, STP);
         }
       }
       // every wave's read-back is done before any wave's DMA reuses the buffer
@@ -764,9 +764,9 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict_
           const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
           const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
           const uint32_t oy = ok ? (uint32_t)(((int64_t)mr * ep.ld_act + f) * 2) : 0x80000000u;
-          __builtin_amdgcn_raw_buffer_store_b128(pair16(g2[0], g2[1]), crs, og, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(pair16(u2[0], u2[1]), crs, ou, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(pair16(y2[0], y2[1]), ars, oy, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(pair16(g2[0], g2[1]), crs, og, 0, STP);
+          __builtin_amdgcn_raw_buffer_store_b128(pair16(u2[0], u2[1]), crs, ou, 0, STP);
+          __builtin_amdgcn_raw_buffer_store_b128(pair16(y2[0], y2[1]), ars, oy, 0, STP);
         }
       }
     } else {  // EPI_DSWIGLU
@@ -816,7 +816,7 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict_
 // workgroup) grid.  Measured against hipBLASLt on the Llama-150M shapes: docs/DESIGN.md §6.
 int g_variant = [] {
   const char* e = getenv("ND_GEMM_VARIANT");
-  return e ? atoi(e) : 7;
+  return e ? atoi(e) : 5;
 }();
 
 // tile grouping of the 4-wave kernels (see coords()); ND_GEMM_GROUP_M or nd_gemm_set_group_m
@@ -847,15 +847,16 @@ int launch_s(const void* A, const void* B, void* C, int M, int N, int K, int64_t
     hipLaunchKernelGGL((gemm_nt_kernel<EPI, HD, SCHED>), dim3(tiles), dim3(512), lds, s, (const bf16_t*)A,
                        (const bf16_t*)B, (bf16_t*)C, M, N, K, lda, ldb, ldc, ep);
   } else {
-    constexpr bool P = SCHED >= 3 && SCHED != 7;
+    constexpr bool P = SCHED >= 3 && SCHED != 7 && SCHED != 8 && SCHED != 9;
     constexpr int Z = SCHED == 4 ? 1 : SCHED >= 5 ? 2 : 0;
+    constexpr int STPC = SCHED == 9 ? 0 : 2;  // C-store cache policy: nt (aux 2; +5 % over plain stores, profiles/r2_gemm_ab.md); 9 = plain (A/B)
     constexpr int AB = SCHED >= 10 ? SCHED - 10 : 0;  // ablation builds (profiling only)
     constexpr int LDK = SCHED == 6 ? 1 : 0;            // buffer_load ... lds instead of global_load_lds
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm4_kernel<EPI, HD, P, Z, AB, LDK>),
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm4_kernel<EPI, HD, P, Z, AB, LDK, STPC>),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (attr != hipSuccess) return (int)attr;
     const int grid = P ? (tiles < num_cus() ? tiles : num_cus()) : tiles;
-    hipLaunchKernelGGL((gemm4_kernel<EPI, HD, P, Z, AB, LDK>), dim3(grid), dim3(256), lds, s, (const bf16_t*)A,
+    hipLaunchKernelGGL((gemm4_kernel<EPI, HD, P, Z, AB, LDK, STPC>), dim3(grid), dim3(256), lds, s, (const bf16_t*)A,
                        (const bf16_t*)B, (bf16_t*)C, M, N, K, lda, ldb, ldc, ep, g_group_m);
   }
   ND_LAUNCH_CHECK();
@@ -879,6 +880,8 @@ int launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t l
     case 5: return launch_s<EPI, HD, 5>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
     case 6: return launch_s<EPI, HD, 6>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
     case 7: return launch_s<EPI, HD, 7>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 8: return launch_s<EPI, HD, 8>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 9: return launch_s<EPI, HD, 9>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
 #ifdef ND_GEMM_ABLATION
     case 11: return launch_s<EPI, HD, 11>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
     case 12: return launch_s<EPI, HD, 12>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
@@ -902,7 +905,7 @@ bool shapes_ok(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
 // GEMM schedule variant for A/B runs (see g_variant); returns the previous one
 ND_API int nd_gemm_set_variant(int v) {
   const int old = g_variant;
-  if ((v >= 0 && v <= 7) || (v > 10 && v < 20)) g_variant = v;
+  if ((v >= 0 && v <= 9) || (v > 10 && v < 20)) g_variant = v;
   return old;
 }
 

@@ -195,10 +195,14 @@ class LlamaForCausalLM:
                                self._g(p + "post_attention_layernorm.weight"), eps, cdt,
                                q8=q_gu, q8_bwd=self._q8(f"{i}.o", grad=True))
         gn = self._gu_names[i]
-        gu = self._linear(f"{i}.gu", y, self._fused(gn, "shadow"), self._fused(gn, "grad"),
-                          q_gu.out if q_gu is not None else None)
+        w_gu = self._fused(gn, "shadow")
         q_down = self._q8(f"{i}.down")
-        act = ops.swiglu(gu, q8=q_down, q8_bwd=self._q8(f"{i}.gu", grad=True))
+        if self.fp8 is None and ops.linear_swiglu_supported(y, w_gu):
+            # own GEMM with SwiGLU in its epilogue (ops/linear.py LinearSwiGLUFn)
+            act = ops.linear_swiglu(y, w_gu, self._fused(gn, "grad"), self._wt(f"{i}.gu", w_gu))
+        else:
+            gu = self._linear(f"{i}.gu", y, w_gu, self._fused(gn, "grad"), q_gu.out if q_gu is not None else None)
+            act = ops.swiglu(gu, q8=q_down, q8_bwd=self._q8(f"{i}.gu", grad=True))
         m = self._linear(f"{i}.down", act, self._w(p + "mlp.down_proj.weight"),
                          self._g(p + "mlp.down_proj.weight"), q_down.out if q_down is not None else None)
         return m, h

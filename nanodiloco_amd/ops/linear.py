@@ -160,3 +160,64 @@ class LinearFn(torch.autograd.Function):
 
 def linear(x: torch.Tensor, w: torch.Tensor, gw: torch.Tensor, wt: torch.Tensor = None) -> torch.Tensor:
     return LinearFn.apply(x, w, gw, wt)
+
+
+_FUSED_SWIGLU = {"enabled": False}
+
+
+def set_fused_swiglu(enabled: bool) -> None:
+    """gate|up projection + SwiGLU as one own-GEMM launch with the activation in its epilogue
+    (``LinearSwiGLUFn``) vs the tuned hipBLASLt GEMM + ``swiglu_fwd`` kernel (default).  Off by
+    default: 1.05-1.08x in isolation against untuned hipBLASLt, but -0.9 % end to end against the
+    pre-tuned table (bench.py --fused-swiglu 1: 731k vs 738k tok/s, 2 interleaved rounds)."""
+    _FUSED_SWIGLU["enabled"] = bool(enabled)
+
+
+def fused_swiglu_enabled() -> bool:
+    return _FUSED_SWIGLU["enabled"]
+
+
+def linear_swiglu_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    from .gemm import nt_supported
+    return (_FUSED_SWIGLU["enabled"] and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2
+            and nt_supported(x, w) and (w.shape[0] // 2) % 8 == 0)
+
+
+class LinearSwiGLUFn(torch.autograd.Function):
+    """act = silu(x W_g^T) * (x W_u^T) for the fused [W_gate; W_up] weight: the own projection GEMM
+    (csrc/gemm.hip, EPI_SWIGLU) writes gu = [gate | up] (the backward's input) and act from its
+    accumulators -- no separate SwiGLU pass over gu (measured 1.05-1.08x the hipBLASLt GEMM +
+    swiglu_fwd pair, profiles/r2_gemm_ab.md).  Backward: ``nd_swiglu_bwd`` -> the usual dgrad /
+    wgrad of the fused projection (ops/linear.py semantics: W^T copy, side-stream wgrad)."""
+
+    @staticmethod
+    def forward(ctx, x, w, gw, wt=None):
+        from .gemm import gemm_nt_swiglu
+        gu, act = gemm_nt_swiglu(x, w)
+        ctx.save_for_backward(x, w if wt is None else wt, gu)
+        ctx.gw = gw
+        ctx.transposed = wt is not None
+        return act
+
+    @staticmethod
+    def backward(ctx, dact):
+        x, w, gu = ctx.saved_tensors
+        dact = dact.contiguous()
+        n, f2 = gu.shape
+        dgu = torch.empty_like(gu)
+        _ext.check(_ext.lib().nd_swiglu_bwd(_ext.ptr(dact), _ext.ptr(gu), _ext.ptr(dgu), _ext.dtcode(gu), n, f2 // 2,
+                                            _ext.stream_ptr(gu.device)), "nd_swiglu_bwd")
+        dx = None
+        if ctx.needs_input_grad[0]:
+            library_gemm_fence(dgu.device)
+            dx = torch.mm(dgu, w.t()) if ctx.transposed else torch.mm(dgu, w)
+        if ctx.gw is not None:
+            if _OVERLAP["enabled"]:
+                _wgrad_on_side_stream(ctx.gw, dgu, x)
+            else:
+                wgrad_accumulate(ctx.gw, dgu, x)
+        return dx, None, None, None
+
+
+def linear_swiglu(x: torch.Tensor, w: torch.Tensor, gw: torch.Tensor, wt: torch.Tensor = None) -> torch.Tensor:
+    return LinearSwiGLUFn.apply(x, w, gw, wt)
