@@ -327,14 +327,27 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
                                                           float* __restrict__ LSE, int B, int nh, int nkv, int T,
                                                           int64_t ld, int64_t ldo, float scale,
                                                           const float* __restrict__ cosT, const float* __restrict__ sinT,
-                                                          const int* __restrict__ KS) {
+                                                          const int* __restrict__ KS, float thr, int order) {
   constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * BN * HD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * BN * HD];
 
   const int nqb = (T + 127) / 128, bh_count = B * nh;
-  const int qb = nqb - 1 - (int)(blockIdx.x / bh_count);  // longest causal rows first
-  const int bh = blockIdx.x % bh_count;
+  // order 0: q-block major (longest causal rows of every head first); 1: the q-blocks of one
+  // (batch, head) run together on one XCD, so its K/V tiles are fetched from HBM once and re-read from L2
+  int qb, bh;
+  if (order) {
+    // every q-block of every query head sharing one (batch, kv head) -- one K/V stream -- in one
+    // contiguous id range, longest rows first inside it
+    const int rep = nh / nkv, grp = nqb * rep;
+    const int id = xcd_remap(blockIdx.x, nqb * bh_count);
+    const int gi = id / grp, wi = id % grp;
+    qb = nqb - 1 - wi / rep;
+    bh = (gi / nkv) * nh + (gi % nkv) * rep + wi % rep;
+  } else {
+    qb = nqb - 1 - (int)(blockIdx.x / bh_count);  // longest causal rows first
+    bh = blockIdx.x % bh_count;
+  }
   const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
   const int ks = PAD ? KS[b] : 0;  // PAD (left-padded batch): keys < ks are masked for every query
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
@@ -419,10 +432,14 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
       mx = pair_max32(mx) * c;  // raw-score max -> log2 domain (c > 0)
-      const float mnew = fmaxf(m, mx);
+      // deferred max (guide T13): the running max moves only when the tile's max exceeds it by more
+      // than thr (log2 units), so p <= 2^thr and the O rescale below is skipped on almost every tile.
+      // Both lanes of a query pair see the same m / mx, so l and O get one consistent factor.
+      const bool upd = mx > m + thr;
+      const float mnew = upd ? mx : m;
       // a row with no visible key yet (a left-pad query: every key masked) keeps p = 0, l = 0
       const float mref = (PAD && mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = fexp2(m - mref);
+      const float alpha = upd ? fexp2(m - mref) : 1.f;
       m = mnew;
       float rs = 0.f;
 #pragma unroll
@@ -513,14 +530,23 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
                                                              const bf16_t* __restrict__ O = nullptr,
                                                              float* __restrict__ NL = nullptr,
                                                              float* __restrict__ ND = nullptr,
-                                                             const int* __restrict__ KS = nullptr) {
+                                                             const int* __restrict__ KS = nullptr, int order = 0) {
   constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * BN * HD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * BN * HD];
 
   const int nqb = (T + 127) / 128, bh_count = B * nh;
-  const int qb = nqb - 1 - (int)(blockIdx.x / bh_count);
-  const int bh = blockIdx.x % bh_count;
+  int qb, bh;
+  if (order) {  // see attn_fwd_kernel
+    const int rep = nh / nkv, grp = nqb * rep;
+    const int id = xcd_remap(blockIdx.x, nqb * bh_count);
+    const int gi = id / grp, wi = id % grp;
+    qb = nqb - 1 - wi / rep;
+    bh = (gi / nkv) * nh + (gi % nkv) * rep + wi % rep;
+  } else {
+    qb = nqb - 1 - (int)(blockIdx.x / bh_count);
+    bh = blockIdx.x % bh_count;
+  }
   const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
   const int ks = PAD ? KS[b] : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
@@ -666,7 +692,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
                                                                int64_t ld, int64_t ldo, float scale,
                                                                const float* __restrict__ cosT,
                                                                const float* __restrict__ sinT,
-                                                               const int* __restrict__ KS) {
+                                                               const int* __restrict__ KS, int order) {
   constexpr int BQ = 64, NT = HD / 16, NO = HD / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Qs[2 * BQ * HD];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[2 * BQ * HD];
@@ -674,8 +700,15 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
   __shared__ __attribute__((aligned(16))) float del_s[2 * BQ];
 
   const int nkb = (T + 127) / 128, bk_count = B * nkv, rep = nh / nkv;
-  const int kb = (int)(blockIdx.x / bk_count);  // small kb = longest query range: dispatched first
-  const int bk = blockIdx.x % bk_count;
+  int kb, bk;  // order 1: the key blocks of one (batch, kv head) together on one XCD (Q / dO from L2)
+  if (order) {
+    const int id = xcd_remap(blockIdx.x, nkb * bk_count);
+    bk = id / nkb;
+    kb = id % nkb;
+  } else {
+    kb = (int)(blockIdx.x / bk_count);  // small kb = longest query range: dispatched first
+    bk = blockIdx.x % bk_count;
+  }
   const int b = bk / nkv, kvh = bk % nkv;
   const int ks = PAD ? KS[b] : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
@@ -808,21 +841,33 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
 }
 
 // ------------------------------------------------------------------------------------ launchers
+// grid order of the attention kernels (see attn_fwd_kernel); ND_ATTN_ORDER=0/1 for A/B
+static int attn_order() {
+  const char* e = getenv("ND_ATTN_ORDER");
+  return e ? atoi(e) : 1;
+}
+// dK/dV: grouping the key blocks of one (batch, kv head) measured -6 % (fwd+bwd) with MHA but +3 %
+// with GQA 32/4 (the group's query heads then stream Q / dO rep times per key block): MHA only
+static int dkdv_order(int nh, int nkv) { return attn_order() && nh == nkv; }
+
 template <int HD, bool PAD>
 static int fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, int B, int nh, int nkv, int T,
                       int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, const int* ks,
                       hipStream_t s) {
   const int nqb = (T + 127) / 128;
   const dim3 g(nqb * B * nh), b(256);
+  // deferred-max threshold (log2 units; ND_ATTN_THR for A/B, 0 = move the max on every increase)
+  const char* te = getenv("ND_ATTN_THR");
+  const float thr = te ? (float)atof(te) : 8.f;
   if (cosT)
     hipLaunchKernelGGL((attn_fwd_kernel<HD, true, false, PAD>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                       (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
+                       (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr, attn_order());
   else if (T % 64 == 0 && !(getenv("ND_ATTN_FWD") && getenv("ND_ATTN_FWD")[0] == 'r'))
     hipLaunchKernelGGL((attn_fwd_kernel<HD, false, true, PAD>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
+                       (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr, attn_order());
   else
     hipLaunchKernelGGL((attn_fwd_kernel<HD, false, false, PAD>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                       (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
+                       (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr, attn_order());
   ND_LAUNCH_CHECK();
 }
 
@@ -888,7 +933,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ NL, const float* __restrict__ ND, bf16_t* __restrict__ dK,
     bf16_t* __restrict__ dV, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
-    const float* __restrict__ cosT, const float* __restrict__ sinT, const int* __restrict__ KS) {
+    const float* __restrict__ cosT, const float* __restrict__ sinT, const int* __restrict__ KS, int order) {
   constexpr int NT = HD / 16, NO = HD / 32;
   constexpr int CPR = HD / 8;              // 16-B chunks per row
   constexpr int RPI = 64 / CPR;            // rows per 1-KiB DMA wave-instruction
@@ -898,9 +943,16 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
   __shared__ __attribute__((aligned(16))) float lse_s[2 * BQ];
   __shared__ __attribute__((aligned(16))) float del_s[2 * BQ];
 
-  const int bk_count = B * nkv, rep = nh / nkv;
-  const int kb = (int)(blockIdx.x / bk_count);
-  const int bk = blockIdx.x % bk_count;
+  const int bk_count = B * nkv, rep = nh / nkv, nkb = (T + 127) / 128;
+  int kb, bk;  // see attn_bwd_dkdv_kernel
+  if (order) {
+    const int id = xcd_remap(blockIdx.x, nkb * bk_count);
+    bk = id / nkb;
+    kb = id % nkb;
+  } else {
+    kb = (int)(blockIdx.x / bk_count);
+    bk = blockIdx.x % bk_count;
+  }
   const int b = bk / nkv, kvh = bk % nkv;
   const int ks = PAD ? KS[b] : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
@@ -1052,24 +1104,24 @@ static void bwd_launch_t(const void* q, const void* k, const void* v, const void
     if (!(bq && bq[0] == '6') && T % 128 == 0)
       hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                          (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
-                         (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
+                         (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
     else
       hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 64, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                          (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
-                         (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
+                         (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
   } else {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, ROPE, ROPE_OUT, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,
-                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
+                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
   }
   if (dma)
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT, !ROPE, false, PAD>), dim3(nb * B * nh), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,
-                       (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, nullptr, nullptr, nullptr, ks);
+                       (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, nullptr, nullptr, nullptr, ks, attn_order());
   else
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, ROPE, ROPE_OUT, false, false, PAD>), dim3(nb * B * nh), dim3(256), 0, s, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, nh, nkv,
-                       T, ld, ldo, scale, cosT, sinT, nullptr, nullptr, nullptr, ks);
+                       T, ld, ldo, scale, cosT, sinT, nullptr, nullptr, nullptr, ks, attn_order());
 }
 
 // rope_mode 0: no RoPE; 1: q/k are RAW projections -- rotated on load, dq/dk un-rotated on store;
@@ -1123,15 +1175,15 @@ static int bwd_fused_launch(const void* q, const void* k, const void* v, const v
   float *nl = ws, *nd = ws + n;
   hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, ROPE_OUT, true, true, PAD>), dim3(nb * B * nh), dim3(256), 0, s,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
-                     (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks);
+                     (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks, attn_order());
   if (T % 128 == 0)
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
-                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
+                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
   else
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 64, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
-                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks);
+                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
   ND_LAUNCH_CHECK();
 }
 

@@ -450,6 +450,156 @@ __global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restr
 
 
 
+
+// ---------------------------------------------------------------------------------------------
+// 4-wave variant (ND_WGRAD_VARIANT=4w; same 256 x 256 tile, LDS image and split-K plan): each wave
+// owns a 128 x 128 quadrant = 4 x 4 v_mfma_f32_32x32x16_bf16 accumulators (256 AGPRs), one wave per
+// SIMD.  The MFMAs are inline asm with tied "+a" accumulators (hipcc would otherwise shuffle a
+// 256-register accumulator set through VGPR copies: csrc/gemm.hip), 16 transposing fragment reads
+// per 16 MFMAs (vs 12 per 8 with the 8-wave split), and the LDS-DMA pieces of tile k+2 are issued
+// between the MFMAs of k-step 3 of tile k and k-step 0 of tile k+1 instead of as one burst.
+// K-tile schedule (4 k-steps of 16): ks0..ks2 read the next k-step's fragments under their MFMAs;
+// after ks2 one vmcnt(0) + barrier (tile k+1 landed everywhere, buffer k&1 read by everyone);
+// ks3 reads tile k+1's ks0 fragments.
+namespace {
+__device__ __forceinline__ void mfma32a(const bf16x8& a, const bf16x8& b, f32x16& c) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma32_drain() { asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 3" ::: "memory"); }
+
+}  // namespace
+
+__global__ void __launch_bounds__(256, 1) wgrad4_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                        float* __restrict__ C, float* __restrict__ slab, int M, int N,
+                                                        int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
+                                                        int kchunk) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  constexpr int TA = BK3 * BM2, TB = BK3 * BN2;  // elements per operand tile
+  const int tn_count = (N + BN2 - 1) / BN2;
+  const int tiles = ((M + BM2 - 1) / BM2) * tn_count;
+  const int id = xcd_remap(blockIdx.x, tiles * S);
+  const int split = id / tiles, tile = id % tiles;
+  const int m0 = (tile / tn_count) * BM2, n0 = (tile % tn_count) * BN2;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int wm = w >> 1, wn = w & 1;  // 2 x 2 waves, 128 x 128 each
+  const int wr = __builtin_amdgcn_readfirstlane(w);
+
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x16{};
+
+  const int nk = kend > kbeg ? (kend - kbeg + BK3 - 1) / BK3 : 0;
+  // per-lane DMA offsets: wave w moves row pairs w + 4 it (it = 0..7) of each 64 x 256 operand tile;
+  // (row & 3) == (2 w + rp) & 3 for every it, so one swizzled column per lane serves all pieces
+  const int rp = lane >> 5;
+  const int csw = (lane & 31) ^ (((2 * w + rp) & 3) << 2);
+  int cola = m0 + csw * 8, colb = n0 + csw * 8;
+  cola = cola < M ? cola : M - 8;
+  colb = colb < N ? colb : N - 8;
+  const uint32_t va = (uint32_t)(((int64_t)rp * lda + cola) * 2);
+  const uint32_t vb = (uint32_t)(((int64_t)rp * ldb + colb) * 2);
+  const uint32_t lds_base = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)smem);
+  // piece j (0-7: A pair w + 4j, 8-15: B pair w + 4(j - 8)) of full tile kt into its buffer
+  auto piece = [&](int kt, int j) __attribute__((always_inline)) {
+    const int k0 = kbeg + kt * BK3;
+    const uint32_t tb = lds_base + (uint32_t)((kt & 1) * (TA + TB) * 2);
+    const int pr = wr + 4 * (j & 7);
+    if (j < 8) glds16s(A + (int64_t)(k0 + 2 * pr) * lda, va, tb + (uint32_t)(pr * 1024));
+    else glds16s(B + (int64_t)(k0 + 2 * pr) * ldb, vb, tb + (uint32_t)(TA * 2 + pr * 1024));
+  };
+  // host guarantees K % 64 == 0 (and kchunk % 64 == 0): every tile is full, streamed by LDS-DMA
+  auto stage_all = [&](int kt) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) piece(kt, j);
+  };
+  if (nk == 0) return;  // (S is planned so every split has work; nothing to write otherwise)
+  stage_all(0);
+  if (nk > 1) stage_all(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  bf16x8 fa0[4], fb0[4], fa1[4], fb1[4];
+  auto rd = [&](const bf16_t* a_t, const bf16_t* b_t, int ks, bf16x8* fa, bf16x8* fb, int i) __attribute__((always_inline)) {
+    fb[i] = frag2(b_t, ks * 16, wn * 128 + i * 32, g, i16);
+    fa[i] = frag2(a_t, ks * 16, wm * 128 + i * 32, g, i16);
+  };
+  {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rd(smem, smem + TA, 0, fa0, fb0, i);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16_t* a_t = smem + (kt & 1) * (TA + TB);
+    const bf16_t* b_t = a_t + TA;
+    const bool dma2 = kt + 2 < nk;                   // tile kt+2: A pieces in this ks3, B pieces in the next ks0
+    const bool dma1_late = kt >= 1 && kt + 1 < nk;   // B pieces of tile kt+1 (its A pieces went in ks3 of kt-1)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this k-step's fragments
+    // ---- ks0 (+ B pieces of tile kt+1 when it streams by DMA)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      if (dma1_late) { piece(kt + 1, 8 + 2 * a); piece(kt + 1, 9 + 2 * a); }
+      rd(a_t, b_t, 1, fa1, fb1, a);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mfma32a(fa0[a], fb0[b], acc[a][b]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- ks1
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      rd(a_t, b_t, 2, fa0, fb0, a);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mfma32a(fa1[a], fb1[b], acc[a][b]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- ks2
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      rd(a_t, b_t, 3, fa1, fb1, a);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mfma32a(fa0[a], fb0[b], acc[a][b]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // tile kt+1 has landed (this wave's DMA), everyone's reads of buffer kt&1 are done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- ks3: A pieces of tile kt+2 and tile kt+1's ks0 fragments under the MFMAs
+    const bf16_t* an = smem + ((kt + 1) & 1) * (TA + TB);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      if (dma2) { piece(kt + 2, 2 * a); piece(kt + 2, 2 * a + 1); }
+      rd(an, an + TA, 0, fa0, fb0, a);  // past the split's end: reads unused LDS
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mfma32a(fa1[a], fb1[b], acc[a][b]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  mfma32_drain();
+  float* out = S == 1 ? C : slab + (int64_t)split * M * N;
+  const int64_t ldo = S == 1 ? ldc : N;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int n = n0 + wn * 128 + b * 32 + c32;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M) {
+          float* p = out + (int64_t)m * ldo + n;
+          if (S == 1) *p += acc[a][b][r];
+          else *p = acc[a][b][r];
+        }
+      }
+    }
+}
+
 // C[m][n] += sum_s slab[s][m][n]   (fixed summation order)
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ C, int M,
                                                           int N, int64_t ldc, int S) {
@@ -512,11 +662,20 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
   // BK=32 ring with counted vmcnt, a 16x16x32-MFMA version and a quadrant-phase pipeline -- all
   // 3-15 % slower than this kernel on the Llama-150M shapes.)
   const char* ev = getenv("ND_WGRAD_VARIANT");
-  const int variant = (ev && ev[0] == 'r') ? 1 : (ev && ev[0] == 'n') ? 4 : 0;
+  const int variant = (ev && ev[0] == 'r') ? 1 : (ev && ev[0] == 'n') ? 4 : (ev && ev[0] == '4') ? 5 : 0;
   // the sched_group_barrier interleave (MFMA / 2 transposing reads) is opt-in ("dmas"): measured
   // 4-13 % SLOWER per kernel than the compiler's own schedule at 32k and 64k tokens, -1.7 % e2e
   const bool sched = ev && ev[0] == 'd' && ev[3] == 's';
-  if (large && variant == 4) {  // "nodma": compute-only diagnostic
+  if (large && variant == 5 && M >= 8 && N >= 8 && K % BK3 == 0) {  // "4w": 4-wave, AGPR-pinned accumulators
+    const int kchunk = ((K + S - 1) / S + BK3 - 1) / BK3 * BK3;
+    const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
+    const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB
+    static const hipError_t attr4 = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad4_kernel),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)attr4;
+    hipLaunchKernelGGL(wgrad4_kernel, dim3(tiles * S), dim3(256), lds, s, (const bf16_t*)A, (const bf16_t*)B, C, slab,
+                       M, N, K, lda, ldb, ldc, S, kchunk);
+  } else if (large && variant == 4) {  // "nodma": compute-only diagnostic
     const int kchunk = ((K + S - 1) / S + BK3 - 1) / BK3 * BK3;
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);
