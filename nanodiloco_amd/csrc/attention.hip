@@ -846,9 +846,12 @@ static int attn_order() {
   const char* e = getenv("ND_ATTN_ORDER");
   return e ? atoi(e) : 1;
 }
-// dK/dV: grouping the key blocks of one (batch, kv head) measured -6 % (fwd+bwd) with MHA but +3 %
-// with GQA 32/4 (the group's query heads then stream Q / dO rep times per key block): MHA only
-static int dkdv_order(int nh, int nkv) { return attn_order() && nh == nkv; }
+// dK/dV: grouping the key blocks of one (batch, kv head) is +3 % with GQA 32/4 in isolation and
+// +1.8 % inside the Llama-150M step (rocprof): off by default (ND_ATTN_DKDV_ORDER=1 for A/B)
+static int dkdv_order(int nh, int nkv) {
+  const char* e = getenv("ND_ATTN_DKDV_ORDER");
+  return e ? atoi(e) && nh == nkv : 0;
+}
 
 template <int HD, bool PAD>
 static int fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, int B, int nh, int nkv, int T,
