@@ -78,6 +78,8 @@ def parse():
                     help="gate|up GEMM with SwiGLU in the own GEMM's epilogue (1) or hipBLASLt + swiglu kernel (0)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
     ap.add_argument("--fp8-wgrad", action="store_true", help="with --fp8: weight-gradient GEMM in fp8 too")
+    ap.add_argument("--fp8-gemm", default="hipblaslt", choices=["hip", "hipblaslt"],
+                    help="with --fp8: forward / input-gradient fp8 GEMMs on our MFMA kernel or hipBLASLt")
     ap.add_argument("--fp8-fused-quant", type=int, default=1, choices=[0, 1],
                     help="with --fp8: operand quantisation fused into the producing kernels (0: separate casts)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
@@ -94,6 +96,7 @@ def main():
     if a.fp8:
         from nanodiloco_amd.ops import fp8 as _fp8
         _fp8.set_fused_quant(bool(a.fp8_fused_quant))
+        _fp8.set_fp8_gemm(a.fp8_gemm)
     if a.wgrad_variant:
         os.environ["ND_WGRAD_VARIANT"] = a.wgrad_variant
     env = init_distributed(a.backend, a.inner_dp)
@@ -232,6 +235,7 @@ def main():
             "tuned_gemm": enable_tuned_gemms(env.device) if env.device.type == "cuda" and not a.no_tuned_gemm else False,
             "wgrad_overlap": ops.wgrad_overlap_enabled(),
             "fused_swiglu_gemm": ops.fused_swiglu_enabled(),
+            "fp8_gemm": a.fp8_gemm if a.fp8 else None,
             "dgrad_transposed": ops.dgrad_transposed_enabled(),
             "ops": ops.get_backend() if a.ops != "auto" else ("hip" if env.device.type == "cuda" else "torch"),
         }

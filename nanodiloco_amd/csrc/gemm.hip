@@ -474,7 +474,6 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict_
                                                        int64_t ldb, int64_t ldc, Epi ep, int GM) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   constexpr int tcols = EPI == EPI_SWIGLU ? 128 : TN;
-  constexpr bool EPI_LDS = EPI == EPI_STORE || EPI == EPI_ROPE;  // C tile re-laid out through LDS
   constexpr int HS = SWZ == 2 ? HALF_P : HALF;  // elements per half-tile
   constexpr int BS = 4 * HS;                     // elements per K-tile buffer
   const int tn = (N + tcols - 1) / tcols, tiles = ((M + TM - 1) / TM) * tn;
@@ -620,8 +619,8 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict_
       // K-tile g + 1 must have landed.  Right after an epilogue its (fixed number of) stores were
       // issued after that DMA and may stay in flight
       if (EPI != EPI_DSWIGLU && kt == 0 && lt > 0) {
+        // (K-tile g + 1 was staged during the previous tile's last k-step, before those stores)
         if constexpr (EPI == EPI_SWIGLU) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-        else if (g + 1 < total) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");  // 32 stores + K-tile g+1's DMA
         else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -636,11 +635,11 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict_
     // cycles, hidden behind the MFMAs already in the pipe (a burst of 16 would idle the SIMD)
     const bf16_t* an = smem + (buf ^ 1) * BS + wm * HS;
     const bf16_t* bn = smem + (buf ^ 1) * BS + (2 + wn) * HS;
-    // an LDS-staged epilogue needs this buffer after the tile's last K-tile: its DMA then waits
-    const bool stage_now = more2 && !(EPI_LDS && kt == nk - 1);
+    // (the C epilogue stages through its own LDS region, so the stream never pauses at a tile end)
+    const bool stage_now = more2;
 #pragma unroll
     for (int a = 0; a < 8; ++a) {
-      if (stage_now && !(ABL & 1)) {  // ABL: ablation builds for profiling only (wrong results)
+      if (stage_now && !(ABL & 1) && LD != 2) {  // ABL: ablation builds for profiling only (wrong results)
         stage_piece(buf, a);
         stage_piece(buf, 8 + a);
       }
@@ -649,14 +648,17 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict_
         fa0[a] = fragz<SWZ>(an, a * 16 + ar0, kq);
       }
 #pragma unroll
-      for (int b = 0; b < 8; ++b) mfma16a(fb1[b], fa1[a], acc[a][b]);
+      for (int b = 0; b < 8; ++b) {
+        mfma16a(fb1[b], fa1[a], acc[a][b]);
+        // LD 2: the group's two DMA pieces after its 2nd and 6th MFMA (issue stalls overlap MFMAs)
+        if (LD == 2 && stage_now && (b == 1 || b == 5)) stage_piece(buf, (b == 1 ? 0 : 8) + a);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if (stage_now) advance();
   }
     mfma_drain();
     const int c_tile = first + lt * G;
-    const int gl = lt * nk + nk - 1;  // stream position of this tile's last K-tile
     // ---------------- epilogue of tile c_tile
     int m0, n0;
     coords(c_tile, m0, n0);
@@ -667,8 +669,8 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int b = 0; b < 8; ++b) asm volatile("" ::"a"(acc[a][b]));
     } else if (EPI == EPI_STORE || EPI == EPI_ROPE) {
-      // C through LDS (the K-tile buffer this tile's last step just released), 32 rows of the
-      // wave's 128 x 128 quadrant per pass: v_permlane16_swap pairs the 4-column quads of blocks
+      // C through the wave's own LDS staging region (behind the two K-tile buffers, so the DMA
+      // stream runs on), 16 rows of the wave's 128 x 128 quadrant per pass: v_permlane16_swap pairs the 4-column quads of blocks
       // b, b + 1 into 16-B pieces (ds_write_b128, rows padded to 272 B), then 16 lanes per row read
       // back whole 256-B row segments and store them with buffer_store_dwordx4 -- full 128-B lines
       // per store instead of 16 half-lines.  Out-of-range lanes are dropped by the descriptor (rows
@@ -676,15 +678,13 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict_
       const __amdgpu_buffer_rsrc_t crs = make_rsrc_n(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)(M - m0 < TM ? M - m0 : TM) * ldc * 2));
       const int q = lane >> 4;
       constexpr int RS = 136;  // staging row stride (elements): 256 B + 16 B pad
-      bf16_t* cst = smem + (gl & 1) * BS + w * (32 * RS);
+      bf16_t* cst = smem + 2 * BS + w * (16 * RS);
       const int ccol = n0 + wn * 128 + (lane & 15) * 8;  // read-back: this lane's 8 columns
       const uint32_t coff = ccol < N ? (uint32_t)(ccol * 2) : 0x80000000u;
       constexpr int HALFD = HD / 2;
 #pragma unroll
-      for (int pass = 0; pass < 4; ++pass) {
-#pragma unroll
-        for (int aa = 0; aa < 2; ++aa) {
-          const int a = pass * 2 + aa;
+      for (int a = 0; a < 8; ++a) {
+        {
           // per group of 4 column blocks (one 64-wide head, or two 32-wide ones): RoPE pairs
           // block b with b + HD/32 inside the group; the tables repeat every head
           float4 ct[2], st[2];
@@ -723,23 +723,20 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict_
 #pragma unroll
             for (int b = 0; b < 4; b += 2) {
               const int col = (g4 * 4 + b + (q & 1)) * 16 + (q >> 1) * 8;
-              *reinterpret_cast<u32x4*>(cst + (aa * 16 + (lane & 15)) * RS + col) = pair16(v[b], v[b + 1]);
+              *reinterpret_cast<u32x4*>(cst + (lane & 15) * RS + col) = pair16(v[b], v[b + 1]);
             }
           }
         }
+        asm volatile("" ::: "memory");  // cross-lane LDS exchange: no compiler reordering
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int row = i * 4 + q;  // 0..31 inside this pass
+        for (int i = 0; i < 4; ++i) {
+          const int row = i * 4 + q;  // 0..15 inside this pass
           const u32x4 d = *reinterpret_cast<const u32x4*>(cst + row * RS + (lane & 15) * 8);
-          const int mr = wm * 128 + pass * 32 + row;
+          const int mr = wm * 128 + a * 16 + row;
           __builtin_amdgcn_raw_buffer_store_b128(d, crs, coff == 0x80000000u ? coff : coff + (uint32_t)(mr * ldc * 2), 0, STP);
         }
+        asm volatile("" ::: "memory");
       }
-      // every wave's read-back is done before any wave's DMA reuses the buffer
-      __builtin_amdgcn_s_waitcnt(LGKM0);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (gl + 2 < total && !(ABL & 1)) stage_next(gl & 1);
     } else if (EPI == EPI_SWIGLU) {
       const __amdgpu_buffer_rsrc_t crs = make_rsrc_n(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)(M - m0 < TM ? M - m0 : TM) * ldc * 2));
       const __amdgpu_buffer_rsrc_t ars = make_rsrc_n(ep.act + (int64_t)m0 * ep.ld_act, (uint32_t)((int64_t)(M - m0 < TM ? M - m0 : TM) * ep.ld_act * 2));
@@ -807,16 +804,281 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(const bf16_t* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp8 x fp8 -> bf16 projection GEMM (the --fp8 recipe's forward e4m3 x e4m3 and input-gradient
+// e5m2 x e4m3 GEMMs; replaces torch._scaled_mm).  C = bf16(sa * sb * A . B^T), sa / sb device scalars
+// (the recipe's inverse scales: delayed scaling, no host sync).
+//
+// A K-tile of 128 fp8 = 128 B per row is byte-for-byte the bf16 kernel's 64-element K-tile, so the
+// LDS image, the LDS-DMA staging stream (persistent grid, padded block layout) and the C epilogue
+// path are those of gemm4_kernel<.., PERSIST, SWZ 2>; the operands are addressed as bf16 pairs.
+// The matrix op is v_mfma_scale_f32_32x32x64_f8f6f4 (unit block scales, E8M0 127): twice the
+// cycles of the bf16 32x32x16 at four times the K, i.e. 2x the bf16 rate.  Per wave 128 x 128 =
+// 4 x 4 accumulators of 32 x 32 (256 AGPRs); a 64-B k-step needs 4 + 4 fragments of 32 B per
+// lane (lane l: row l % 32, bytes (l / 32) * 32 + [0, 32) of the step -- A and B use the same
+// byte -> k assignment, so the MFMA's internal K order does not matter), double-buffered exactly
+// like the bf16 kernel's two k-steps.  Accumulator lane l holds token row l % 32 and output
+// columns 8 i + 4 (l / 32) + [0, 4) of its 32-column block (i = 0..3).
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ i32x8 frag8(const bf16_t* half, int row, int kc) {
+  const bf16_t* p = &half[(row & 15) * (BLOCK_P / 2) + (row >> 4) * 64 + kc];
+  const i32x4v lo = *reinterpret_cast<const i32x4v*>(p);
+  const i32x4v hi = *reinterpret_cast<const i32x4v*>(p + 8);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// D += A . B^T with A / B fp8 (CB = format of the first operand, BL = of the second: 0 e4m3,
+// 1 e5m2), unit E8M0 scales (`one` = 0x7F7F7F7F), accumulator pinned to AGPRs as in mfma16a
+template <int CB, int BL>
+__device__ __forceinline__ void mfma32f8(const i32x8& a, const i32x8& b, f32x16& c, int one) {
+  if constexpr (CB == 0 && BL == 0)
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]" : "+a"(c) : "v"(a), "v"(b), "v"(one));
+  else if constexpr (CB == 0 && BL == 1)
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] blgp:1" : "+a"(c) : "v"(a), "v"(b), "v"(one));
+  else if constexpr (CB == 1 && BL == 0)
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:1" : "+a"(c) : "v"(a), "v"(b), "v"(one));
+  else
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:1 blgp:1" : "+a"(c) : "v"(a), "v"(b), "v"(one));
+}
+
+// the same with a zero accumulator input (first k-step of a tile): no per-tile AGPR zeroing
+template <int CB, int BL>
+__device__ __forceinline__ void mfma32f8z(const i32x8& a, const i32x8& b, f32x16& c, int one) {
+  if constexpr (CB == 0 && BL == 0)
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0]" : "=a"(c) : "v"(a), "v"(b), "v"(one));
+  else if constexpr (CB == 0 && BL == 1)
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0] blgp:1" : "=a"(c) : "v"(a), "v"(b), "v"(one));
+  else if constexpr (CB == 1 && BL == 0)
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0] cbsz:1" : "=a"(c) : "v"(a), "v"(b), "v"(one));
+  else
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0] cbsz:1 blgp:1" : "=a"(c) : "v"(a), "v"(b), "v"(one));
+}
+
+// FA / FB: formats of A (tokens) and B (weight); M, N in rows, K / lda / ldb in bf16 PAIRS (fp8 / 2)
+template <int FA, int FB, bool ILV>
+__global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                          bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                          int64_t ldb, int64_t ldc, const float* __restrict__ sa,
+                                                          const float* __restrict__ sb, int GM) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  constexpr int HS = HALF_P, BS = 4 * HS;
+  const int tn = (N + TN - 1) / TN, tmn = (M + TM - 1) / TM, tiles = tmn * tn;
+  const int G = gridDim.x;
+  const int first = xcd_remap(blockIdx.x, G);
+  const int my_tiles = first < tiles ? (tiles - 1 - first) / G + 1 : 0;
+  const int nk = K / TK;
+  const int total = my_tiles * nk;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int wr = __builtin_amdgcn_readfirstlane(w);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)smem);
+  const float scale = sa[0] * sb[0];
+
+  int s_tile = first, s_kt = 0;
+  auto coords = [&](int t, int& m0, int& n0) __attribute__((always_inline)) {
+    if (GM <= 1) {
+      m0 = (t / tn) * TM;
+      n0 = (t % tn) * TN;
+    } else {
+      const int per = GM * tn, grp = t / per, r = t - grp * per;
+      const int gm = (tmn - grp * GM) < GM ? (tmn - grp * GM) : GM;
+      m0 = (grp * GM + r % gm) * TM;
+      n0 = (r / gm) * TN;
+    }
+  };
+  int s_m0, s_n0;
+  coords(s_tile, s_m0, s_n0);
+  uint32_t va[2][4], vb[2][4];
+  auto offsets = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int hr = (w + 4 * p) + 16 * (lane >> 3), lch = lane & 7, r = 128 * h + hr;
+        int ar = s_m0 + r;
+        ar = (ar < M ? ar : M - 1) - s_m0;
+        va[h][p] = (uint32_t)(((int64_t)ar * lda + lch * 8) * 2);
+        int br = s_n0 + r;
+        br = (br < N ? br : N - 1) - s_n0;
+        vb[h][p] = (uint32_t)(((int64_t)br * ldb + lch * 8) * 2);
+      }
+  };
+  offsets();
+  auto stage_piece = [&](int buf, int j) __attribute__((always_inline)) {
+    const uint32_t dst = lds0 + (uint32_t)(buf * BS * 2);
+    const int h = (j >> 2) & 1, p = j & 3;
+    if (j < 8)
+      glds(A + (int64_t)s_m0 * lda + (int64_t)s_kt * TK, va[h][p], dst + (uint32_t)((h * HS) * 2 + (wr + 4 * p) * BLOCK_P));
+    else
+      glds(B + (int64_t)s_n0 * ldb + (int64_t)s_kt * TK, vb[h][p], dst + (uint32_t)(((2 + h) * HS) * 2 + (wr + 4 * p) * BLOCK_P));
+  };
+  auto advance = [&]() __attribute__((always_inline)) {
+    if (++s_kt == nk) {
+      s_kt = 0;
+      s_tile += G;
+      if (s_tile < tiles) {
+        coords(s_tile, s_m0, s_n0);
+        offsets();
+      }
+    }
+  };
+  auto stage_next = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) stage_piece(buf, j);
+    advance();
+  };
+
+  f32x16 acc[4][4];  // written first by mfma32f8z
+  if (total == 0) return;
+  const int one = 0x7F7F7F7F;
+
+  stage_next(0);
+  if (total > 1) {
+    stage_next(1);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  const int r32 = lane & 31, kb = (lane >> 5) * 16;  // kb: element (bf16-pair) offset in a 64-B k-step
+  i32x8 fa0[4], fb0[4], fa1[4], fb1[4];
+  {
+    const bf16_t* at = smem + wm * HS;
+    const bf16_t* bt = smem + (2 + wn) * HS;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) fb0[b] = frag8(bt, b * 32 + r32, kb);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) fa0[a] = frag8(at, a * 32 + r32, kb);
+  }
+  for (int lt = 0; lt < my_tiles; ++lt) {
+    for (int kt = 0; kt < nk; ++kt) {
+      const int g = lt * nk + kt;
+      const int buf = g & 1;
+      const bool more1 = g + 1 < total, more2 = g + 2 < total;
+      const bf16_t* at = smem + buf * BS + wm * HS;
+      const bf16_t* bt = smem + buf * BS + (2 + wn) * HS;
+      __builtin_amdgcn_s_waitcnt(LGKM0);
+      if (kt == 0) {  // first k-step of a tile: the MFMAs start from a zero accumulator
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          fb1[a] = frag8(bt, a * 32 + r32, 32 + kb);
+          fa1[a] = frag8(at, a * 32 + r32, 32 + kb);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) mfma32f8z<FB, FA>(fb0[b], fa0[a], acc[a][b], one);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          fb1[a] = frag8(bt, a * 32 + r32, 32 + kb);
+          fa1[a] = frag8(at, a * 32 + r32, 32 + kb);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) mfma32f8<FB, FA>(fb0[b], fa0[a], acc[a][b], one);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (more1) {
+        if (kt == 0 && lt > 0) {
+          asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // K-tile g + 1 was issued before the 32 stores
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(LGKM0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16_t* an = smem + (buf ^ 1) * BS + wm * HS;
+      const bf16_t* bn = smem + (buf ^ 1) * BS + (2 + wn) * HS;
+      const bool stage_now = more2;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        if constexpr (ILV) {
+          // one LDS-DMA piece after each MFMA: a piece's issue stall overlaps the MFMA before it
+          fb0[a] = frag8(bn, a * 32 + r32, kb);  // past the stream's end: reads unused LDS
+          fa0[a] = frag8(an, a * 32 + r32, kb);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            mfma32f8<FB, FA>(fb1[b], fa1[a], acc[a][b], one);
+            if (stage_now) stage_piece(buf, (b & 1) * 8 + 2 * a + (b >> 1));
+          }
+        } else {
+          if (stage_now) {
+            stage_piece(buf, 2 * a);
+            stage_piece(buf, 2 * a + 1);
+            stage_piece(buf, 8 + 2 * a);
+            stage_piece(buf, 9 + 2 * a);
+          }
+          fb0[a] = frag8(bn, a * 32 + r32, kb);  // past the stream's end: reads unused LDS
+          fa0[a] = frag8(an, a * 32 + r32, kb);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) mfma32f8<FB, FA>(fb1[b], fa1[a], acc[a][b], one);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (stage_now) advance();
+    }
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 7" ::: "memory");  // 16-pass MFMA results -> VALU
+    const int c_tile = first + lt * G;
+    int m0, n0;
+    coords(c_tile, m0, n0);
+    // C through the wave's own LDS staging region (behind the K-tile buffers), in fp32: per pass
+    // 16 rows x 64 columns of two accumulator blocks (the lanes holding those rows write 16-B
+    // pieces straight from the accumulators), then 8 lanes per row read 8 columns back, apply the
+    // scale, round once to bf16 and store whole 128-B lines; every wave issues exactly 32 stores.
+    // (Scaling in registers before the staging made hipcc keep accumulators in VGPRs and spill.)
+    const __amdgpu_buffer_rsrc_t crs = make_rsrc_n(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)(M - m0 < TM ? M - m0 : TM) * ldc * 2));
+    constexpr int RSF = 68;  // fp32 staging row stride (floats): 256 B + 16 B pad
+    float* cst = reinterpret_cast<float*>(smem + 2 * BS) + w * (16 * RSF);
+    const int q8 = lane >> 3;
+#pragma unroll
+    for (int pass = 0; pass < 16; ++pass) {
+      const int a = pass >> 2, bh = ((pass >> 1) & 1) * 2, hh = pass & 1;  // rows hh * 16 + [0, 16)
+      if (((lane >> 4) & 1) == hh) {
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const f32x16& v = acc[a][bh + bb];
+            const int col = bb * 32 + i * 8 + (lane >> 5) * 4;
+            *reinterpret_cast<f32x4*>(cst + (lane & 15) * RSF + col) = f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+          }
+      }
+      // lanes read what other lanes wrote: keep hipcc from reordering the LDS accesses across
+      // (the hardware runs one wave's LDS instructions in order)
+      asm volatile("" ::: "memory");
+      const int ccol = n0 + wn * 128 + bh * 32 + (lane & 7) * 8;
+      const uint32_t coff = ccol < N ? (uint32_t)(ccol * 2) : 0x80000000u;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = i * 8 + q8;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(cst + row * RSF + (lane & 7) * 8);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(cst + row * RSF + (lane & 7) * 8 + 4);
+        const u32x4 d = u32x4{pack2(x0[0] * scale, x0[1] * scale), pack2(x0[2] * scale, x0[3] * scale),
+                              pack2(x1[0] * scale, x1[1] * scale), pack2(x1[2] * scale, x1[3] * scale)};
+        const int mr = wm * 128 + a * 32 + hh * 16 + row;
+        __builtin_amdgcn_raw_buffer_store_b128(d, crs, coff == 0x80000000u ? coff : coff + (uint32_t)(mr * ldc * 2), 0, 2);
+      }
+      asm volatile("" ::: "memory");
+    }
+  }
+}
+
 // Variants (ND_GEMM_VARIANT or nd_gemm_set_variant, for in-process A/B): 0 = 8 waves, four barrier-
 // separated phases per K-tile; 1 = 8 waves, register-pipelined, one barrier per K-tile; 2 = 4 waves of
 // 128 x 128 (one wave per SIMD); 3 = variant 2 as a persistent grid with a cross-tile DMA stream;
 // 4 = variant 3 with the half-swap LDS swizzle (coalesced 64-B DMA source quads); 5 = variant 3 with
 // the padded block layout (whole ascending 128-B rows per DMA lane octet, conflict-free reads);
-// 6 = variant 5 with buffer_load ... lds DMA; 7 (default) = variant 5 on a plain (one tile per
-// workgroup) grid.  Measured against hipBLASLt on the Llama-150M shapes: docs/DESIGN.md §6.
+// 6 = variant 5 with buffer_load ... lds DMA; 7 = variant 5 on a plain (one tile per workgroup)
+// grid; 8 = 5; 9 = 5 with plain C stores; 10 (default) = variant 5 with each k-step-1 DMA piece issued
+// between MFMAs (+1.8 % over 5).  Measured against hipBLASLt on the Llama-150M shapes: docs/DESIGN.md.
 int g_variant = [] {
   const char* e = getenv("ND_GEMM_VARIANT");
-  return e ? atoi(e) : 5;
+  return e ? atoi(e) : 10;
 }();
 
 // tile grouping of the 4-wave kernels (see coords()); ND_GEMM_GROUP_M or nd_gemm_set_group_m
@@ -837,7 +1099,8 @@ int num_cus() {
 template <int EPI, int HD, int SCHED>
 int launch_s(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
              const Epi& ep, hipStream_t s) {
-  const size_t lds = 2 * (size_t)(SCHED >= 5 ? 4 * HALF_P : BUF) * sizeof(bf16_t);  // 128 / 132 KiB
+  // two K-tile buffers (128 / 132 KiB) + the C epilogue's staging rows (4 waves x 16 x 272 B)
+  const size_t lds = (2 * (size_t)(SCHED >= 5 ? 4 * HALF_P : BUF) + 4 * 16 * 136) * sizeof(bf16_t);
   const int tcols = EPI == EPI_SWIGLU ? 128 : TN;
   const int tiles = ((M + TM - 1) / TM) * ((N + tcols - 1) / tcols);
   if constexpr (SCHED <= 1) {
@@ -847,11 +1110,11 @@ int launch_s(const void* A, const void* B, void* C, int M, int N, int K, int64_t
     hipLaunchKernelGGL((gemm_nt_kernel<EPI, HD, SCHED>), dim3(tiles), dim3(512), lds, s, (const bf16_t*)A,
                        (const bf16_t*)B, (bf16_t*)C, M, N, K, lda, ldb, ldc, ep);
   } else {
-    constexpr bool P = SCHED >= 3 && SCHED != 7 && SCHED != 8 && SCHED != 9;
+    constexpr bool P = SCHED >= 3 && SCHED != 7 && SCHED != 8 && SCHED != 9;  // 10: persistent, padded, interleaved DMA
     constexpr int Z = SCHED == 4 ? 1 : SCHED >= 5 ? 2 : 0;
     constexpr int STPC = SCHED == 9 ? 0 : 2;  // C-store cache policy: nt (aux 2; +5 % over plain stores, profiles/r2_gemm_ab.md); 9 = plain (A/B)
-    constexpr int AB = SCHED >= 10 ? SCHED - 10 : 0;  // ablation builds (profiling only)
-    constexpr int LDK = SCHED == 6 ? 1 : 0;            // buffer_load ... lds instead of global_load_lds
+    constexpr int AB = SCHED > 10 ? SCHED - 10 : 0;  // ablation builds (profiling only)
+    constexpr int LDK = SCHED == 6 ? 1 : SCHED == 10 ? 2 : 0;  // 1: buffer_load ... lds; 2: DMA pieces between MFMAs
     static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm4_kernel<EPI, HD, P, Z, AB, LDK, STPC>),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (attr != hipSuccess) return (int)attr;
@@ -882,6 +1145,7 @@ int launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t l
     case 7: return launch_s<EPI, HD, 7>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
     case 8: return launch_s<EPI, HD, 8>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
     case 9: return launch_s<EPI, HD, 9>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    case 10: return launch_s<EPI, HD, 10>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
 #ifdef ND_GEMM_ABLATION
     case 11: return launch_s<EPI, HD, 11>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
     case 12: return launch_s<EPI, HD, 12>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
@@ -900,12 +1164,61 @@ bool shapes_ok(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
   return M > 0 && N > 0 && K > 0 && K % TK == 0 && N % 4 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 &&
          lda >= K && ldb >= K && (int64_t)TM * lda * 2 < (1ll << 31) && (int64_t)TN * ldb * 2 < (1ll << 31);
 }
+int g_f8_variant = [] {
+  const char* e = getenv("ND_GEMM_F8_VARIANT");
+  return e ? atoi(e) : 1;
+}();
+
+template <int FA, int FB, bool ILV>
+int launch_f8_v(const void* A, const void* B, void* C, int M, int N, int K2, int64_t lda2, int64_t ldb2, int64_t ldc,
+              const float* sa, const float* sb, hipStream_t s) {
+  const size_t lds = 2 * (size_t)(4 * HALF_P) * sizeof(bf16_t) + 4 * 16 * 68 * sizeof(float);  // 149 KiB
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm4_f8_kernel<FA, FB, ILV>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return (int)attr;
+  const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  const int grid = tiles < num_cus() ? tiles : num_cus();
+  hipLaunchKernelGGL((gemm4_f8_kernel<FA, FB, ILV>), dim3(grid), dim3(256), lds, s, (const bf16_t*)A, (const bf16_t*)B,
+                     (bf16_t*)C, M, N, K2, lda2, ldb2, ldc, sa, sb, g_group_m);
+  ND_LAUNCH_CHECK();
+}
+// ND_GEMM_F8_VARIANT / nd_gemm_set_f8_variant: 1 (default) = one DMA piece per MFMA in k-step 1,
+// 0 = four pieces ahead of each group of four MFMAs
+template <int FA, int FB>
+int launch_f8(const void* A, const void* B, void* C, int M, int N, int K2, int64_t lda2, int64_t ldb2, int64_t ldc,
+              const float* sa, const float* sb, hipStream_t s) {
+  return g_f8_variant ? launch_f8_v<FA, FB, true>(A, B, C, M, N, K2, lda2, ldb2, ldc, sa, sb, s)
+                      : launch_f8_v<FA, FB, false>(A, B, C, M, N, K2, lda2, ldb2, ldc, sa, sb, s);
+}
 }  // namespace
+
+// fp8 GEMM: C[M, N] (bf16) = sa[0] * sb[0] * A[M, K] . B[N, K]^T with A, B OCP fp8 (fa / fb: 0 = e4m3,
+// 1 = e5m2).  K, lda, ldb in fp8 elements (bytes): K % 128 == 0, lda / ldb % 16 == 0; N % 8 == 0,
+// ldc % 8 == 0; 16-B aligned base pointers.
+ND_API int nd_gemm_nt_f8(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                         int64_t ldc, int fa, int fb, const float* sa, const float* sb, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 128 || lda % 16 || ldb % 16 || N % 8 || ldc % 8 || lda < K || ldb < K ||
+      (int64_t)TM * lda >= (1ll << 31) || (int64_t)TN * ldb >= (1ll << 31) || (int64_t)TM * ldc * 2 >= (1ll << 31) ||
+      fa < 0 || fa > 1 || fb < 0 || fb > 1 || !sa || !sb)
+    return (int)hipErrorInvalidValue;
+  const int K2 = K / 2;
+  const int64_t la = lda / 2, lb = ldb / 2;
+  if (fa == 0 && fb == 0) return launch_f8<0, 0>(A, B, C, M, N, K2, la, lb, ldc, sa, sb, s);
+  if (fa == 1 && fb == 0) return launch_f8<1, 0>(A, B, C, M, N, K2, la, lb, ldc, sa, sb, s);
+  if (fa == 0 && fb == 1) return launch_f8<0, 1>(A, B, C, M, N, K2, la, lb, ldc, sa, sb, s);
+  return launch_f8<1, 1>(A, B, C, M, N, K2, la, lb, ldc, sa, sb, s);
+}
 
 // GEMM schedule variant for A/B runs (see g_variant); returns the previous one
 ND_API int nd_gemm_set_variant(int v) {
   const int old = g_variant;
-  if ((v >= 0 && v <= 9) || (v > 10 && v < 20)) g_variant = v;
+  if ((v >= 0 && v <= 10) || (v > 10 && v < 20)) g_variant = v;
+  return old;
+}
+
+ND_API int nd_gemm_set_f8_variant(int v) {
+  const int old = g_f8_variant;
+  if (v == 0 || v == 1) g_f8_variant = v;
   return old;
 }
 

@@ -1,7 +1,8 @@
 """fp8 inner step (BASELINE config 5): OCP fp8 GEMMs for the decoder projections on gfx950.
 
 Recipe (per-tensor scaling, the common "delayed scaling" scheme):
-* forward  ``y = x @ W^T`` with x, W in e4m3 -> hipBLASLt fp8 GEMM (``torch._scaled_mm``), bf16 out;
+* forward  ``y = x @ W^T`` with x, W in e4m3 -> hipBLASLt (``torch._scaled_mm``, default) or our fp8
+  MFMA GEMM (``gemm.gemm_nt_f8``, ``v_mfma_scale_f32_32x32x64_f8f6f4``; ``set_fp8_gemm("hip")``), bf16 out;
 * dgrad    ``dx = dy @ W`` with dy in e5m2 (range for gradients), W^T in e4m3;
 * wgrad    ``dW = dy^T x`` as an fp8 GEMM too (e5m2 x e4m3, fp32 out, added into the flat fp32 grad
   buffer); its K-major operands dy^T / x^T come from ``nd_fp8_cast_t``, which writes the fp8 tensor
@@ -29,7 +30,7 @@ from typing import Dict, Optional
 import torch
 
 from . import _ext
-from .gemm import wgrad, wgrad_supported
+from .gemm import f8_nt_supported, gemm_nt_f8, wgrad, wgrad_supported
 
 E4M3, E5M2 = 0, 1
 FMAX = {E4M3: 448.0, E5M2: 57344.0}
@@ -38,6 +39,27 @@ TORCH_DT = {E4M3: torch.float8_e4m3fn, E5M2: torch.float8_e5m2}
 
 AMAX_PARTS = 64
 _FUSED = {"enabled": True}
+# hipBLASLt stays the default: our kernel reaches 0.95x of its fp8 GEMMs per shape and costs 2.7 %
+# of the --fp8 step (profiles/r2_fp8_gemm_ab.md)
+_GEMM = {"backend": "hipblaslt"}
+
+
+def set_fp8_gemm(backend: str) -> None:
+    """fp8 forward / input-gradient GEMMs on our MFMA kernel ("hip") or hipBLASLt ("hipblaslt", default)."""
+    if backend not in ("hip", "hipblaslt"):
+        raise ValueError(backend)
+    _GEMM["backend"] = backend
+
+
+def fp8_gemm_backend() -> str:
+    return _GEMM["backend"]
+
+
+def mm8(a8: torch.Tensor, b8: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) -> torch.Tensor:
+    """bf16 sa * sb * a8 . b8^T (a8 [M, K], b8 [N, K] fp8)."""
+    if _GEMM["backend"] == "hip" and f8_nt_supported(a8, b8):
+        return gemm_nt_f8(a8, b8, sa, sb)
+    return torch._scaled_mm(a8, b8.t(), sa, sb, out_dtype=torch.bfloat16)
 
 
 def set_fused_quant(enabled: bool) -> None:
@@ -210,7 +232,7 @@ class Fp8LinearFn(torch.autograd.Function):
                 x8 = recipe.quantize(x, kx, E4M3)
             ctx.save_for_backward(x)
         inv_x = recipe.inv[kx:kx + 1]
-        y = torch._scaled_mm(x8, wq.w8.t(), inv_x, wq.inv, out_dtype=torch.bfloat16)
+        y = mm8(x8, wq.w8, inv_x, wq.inv)
         ctx.gw, ctx.wq, ctx.recipe, ctx.kdy, ctx.inv_x, ctx.wgrad_fp8 = gw, wq, recipe, kdy, inv_x, wgrad_fp8
         return y
 
@@ -226,7 +248,7 @@ class Fp8LinearFn(torch.autograd.Function):
             if dy8 is None:
                 dy8 = r.quantize(dy, k, E5M2)
         inv_dy = r.inv[k:k + 1]
-        dx = torch._scaled_mm(dy8, ctx.wq.wT8.t(), inv_dy, ctx.wq.inv, out_dtype=torch.bfloat16)
+        dx = mm8(dy8, ctx.wq.wT8, inv_dy, ctx.wq.inv)
         if ctx.gw is not None:
             if ctx.wgrad_fp8:
                 # dW[out, in] = dy^T x : mat1 = dy^T (row-major), mat2 = x as column-major [T, in]

@@ -53,6 +53,11 @@ def set_gemm_variant(v: int) -> int:
     return int(_ext.lib().nd_gemm_set_variant(int(v)))
 
 
+def set_gemm_f8_variant(v: int) -> int:
+    """fp8 GEMM schedule (csrc/gemm.hip g_f8_variant, A/B); returns the previous one."""
+    return _ext.lib().nd_gemm_set_f8_variant(int(v))
+
+
 def set_gemm_group_m(g: int) -> int:
     """Tile grouping (m-panels per group) of the 4-wave GEMM variants; 0/1 = row-major tiles."""
     return int(_ext.lib().nd_gemm_set_group_m(int(g)))
@@ -68,6 +73,32 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, variant:
         out = torch.empty(M, N, dtype=a.dtype, device=a.device)
     _ext.check(_ext.lib().nd_gemm_nt(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0), b.stride(0),
                                      out.stride(0), _ext.stream_ptr(a.device)), "nd_gemm_nt")
+    return out
+
+
+_F8_FMT = {torch.float8_e4m3fn: 0, torch.float8_e5m2: 1}
+
+
+def f8_nt_supported(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Shapes / layouts the own fp8 GEMM takes: K % 128, N % 8, row strides % 16, 16-B aligned."""
+    return (a.is_cuda and a.dim() == 2 and b.dim() == 2 and a.dtype in _F8_FMT and b.dtype in _F8_FMT
+            and a.shape[1] == b.shape[1] and a.shape[1] % 128 == 0 and b.shape[0] % 8 == 0
+            and a.stride(1) == 1 and b.stride(1) == 1 and a.stride(0) % 16 == 0 and b.stride(0) % 16 == 0
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+
+
+def gemm_nt_f8(a: torch.Tensor, b: torch.Tensor, scale_a: torch.Tensor, scale_b: torch.Tensor,
+               out: torch.Tensor = None) -> torch.Tensor:
+    """out[M, N] (bf16) = scale_a * scale_b * a[M, K] . b[N, K]^T with a, b OCP fp8 (e4m3 / e5m2) and
+    the scales one-element fp32 device tensors -- the ``torch._scaled_mm(a, b.t(), scale_a, scale_b,
+    out_dtype=bf16)`` contract, on our MFMA kernel (``nd_gemm_nt_f8``)."""
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_nt_f8(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0), b.stride(0),
+                                        out.stride(0), _F8_FMT[a.dtype], _F8_FMT[b.dtype], _ext.ptr(scale_a),
+                                        _ext.ptr(scale_b), _ext.stream_ptr(a.device)), "nd_gemm_nt_f8")
     return out
 
 

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="1,2,3", help="own-kernel schedule variants to A/B (csrc/gemm.hip)")
     ap.add_argument("--only", default="", help="comma list of case-name prefixes")
+    ap.add_argument("--fp8", action="store_true", help="fp8 GEMMs (gemm_nt_f8 vs torch._scaled_mm) instead")
     a = ap.parse_args()
     ops.set_backend("hip")
     M = a.tokens
@@ -51,6 +52,20 @@ def main():
         out = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
         cases.append((name, 2.0 * m * n * k, lambda: G.gemm_nt(x, w, out), lambda: torch.mm(x, w.t(), out=out)))
 
+    def plain8(name, m, n, k, fa=torch.float8_e4m3fn):
+        x8, w8 = r(m, k).to(fa), (r(n, k) * 0.05).to(torch.float8_e4m3fn)
+        sa, sb = torch.ones(1, device="cuda"), torch.ones(1, device="cuda")
+        out = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+        cases.append((name, 2.0 * m * n * k, lambda: G.gemm_nt_f8(x8, w8, sa, sb, out),
+                      lambda: torch._scaled_mm(x8, w8.t(), sa, sb, out_dtype=torch.bfloat16)))
+
+    if a.fp8:
+        e5 = torch.float8_e5m2
+        for nm, n, k in (("qkv", qkv_n, d), ("o", d, nh * hd), ("gu", 2 * F, d), ("down", d, F)):
+            plain8(nm + " fwd8", M, n, k)
+        for nm, n, k in (("qkv", d, qkv_n), ("o", nh * hd, d), ("gu", d, 2 * F), ("down", F, d)):
+            plain8(nm + " dgrad8", M, n, k, e5)
+        a.only = a.only or "qkv fwd8,o fwd8,gu fwd8,down fwd8,qkv dgrad8,o dgrad8,gu dgrad8,down dgrad8"
     plain("qkv fwd", M, qkv_n, d)
     plain("o fwd", M, d, nh * hd)
     plain("gu fwd", M, 2 * F, d)
@@ -106,7 +121,10 @@ def main():
         tb = []
         for _ in range(a.rounds):
             for v in variants:
-                G.set_gemm_variant(specs[v][0])
+                if a.fp8:  # --variants then selects the fp8 kernel's schedule (g_f8_variant)
+                    G.set_gemm_f8_variant(specs[v][0])
+                else:
+                    G.set_gemm_variant(specs[v][0])
                 G.set_gemm_group_m(specs[v][1])
                 to[v].append(timed(ours))
             tb.append(timed(lib))

@@ -68,8 +68,17 @@ def test_fp8_weight_current_scaling(shape):
     assert wq.get(w, version=0) is wq and wq.version == 0
 
 
+@pytest.fixture(params=["hipblaslt", "hip"])
+def fp8_gemm(request):
+    """Both fp8 GEMM backends: hipBLASLt (default) and the own MFMA kernel (csrc/gemm.hip)."""
+    old = fp8.fp8_gemm_backend()
+    fp8.set_fp8_gemm(request.param)
+    yield request.param
+    fp8.set_fp8_gemm(old)
+
+
 @pytest.mark.parametrize("wgrad_fp8", [True, False])
-def test_fp8_linear_close_to_fp32(wgrad_fp8):
+def test_fp8_linear_close_to_fp32(wgrad_fp8, fp8_gemm):
     M, N, K = 2048, 1536, 1024
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
@@ -91,7 +100,7 @@ def test_fp8_linear_close_to_fp32(wgrad_fp8):
     assert torch.isfinite(lin.recipe.scale[:2]).all() and (lin.recipe.scale[:2] > 0).all()
 
 
-def test_fp8_training_tracks_bf16():
+def test_fp8_training_tracks_bf16(fp8_gemm):
     cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=768, num_attention_heads=4,
                                      num_key_value_heads=4, num_hidden_layers=2, vocab_size=512))
     ids = torch.randint(0, 512, (8, 256), device="cuda")

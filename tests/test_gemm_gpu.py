@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True, params=[(1, 0), (3, 4), (4, 0), (5, 3), (6, 4), (7, 0), (7, 4)], ids=lambda v: f"v{v[0]}g{v[1]}")
+@pytest.fixture(autouse=True, params=[(1, 0), (3, 4), (4, 0), (5, 3), (6, 4), (7, 0), (7, 4), (10, 4)], ids=lambda v: f"v{v[0]}g{v[1]}")
 def _hip(hip_lib, request):
     """Every test runs on each schedule variant of the kernel (csrc/gemm.hip g_variant) and on a
     grouped tile order with a short last group (g_group_m = 3)."""
@@ -36,7 +36,8 @@ def rel(a, b):
 
 
 SHAPES = [(256, 256, 64), (1024, 768, 512), (777, 1000, 320), (300, 260, 128), (4096, 3072, 1024),
-          (2048, 1024, 2688), (1024, 5376, 1024), (512, 32000, 1024), (64, 4, 64)]
+          (2048, 1024, 2688), (1024, 5376, 1024), (512, 32000, 1024), (64, 4, 64),
+          (16384, 3072, 1024), (9000, 2056, 512)]  # the last two: several tiles per persistent workgroup
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
