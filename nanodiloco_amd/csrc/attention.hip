@@ -329,10 +329,8 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
                                                           const float* __restrict__ cosT, const float* __restrict__ sinT,
                                                           const int* __restrict__ KS, float thr, int order) {
   constexpr int BN = 64, NT = HD / 16, NO = HD / 32;
-  // DMA: a 3-tile ring (two tiles in flight while one is read); register staging: double buffer
-  constexpr int NB = DMA ? 3 : 2;
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[NB * BN * HD];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[NB * BN * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * BN * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * BN * HD];
 
   const int nqb = (T + 127) / 128, bh_count = B * nh;
   // order 0: q-block major (longest causal rows of every head first); 1: the q-blocks of one
@@ -374,17 +372,15 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
   Stage<BN, HD> sv;
   TileDma<HD, BN> tdma;
   const uint32_t ks_a = lds_addr(Ks), vs_a = lds_addr(Vs);
-  auto dma_issue = [&](int j, int slot) {
-    const uint32_t off = (uint32_t)(slot * BN * HD * 2);
+  auto dma_issue = [&](int j) {
+    const uint32_t off = (uint32_t)((j & 1) * BN * HD * 2);
     tdma.issue(Kb + (int64_t)j * BN * ld, ks_a + off);
     tdma.issue(Vb + (int64_t)j * BN * ld, vs_a + off);
   };
   if constexpr (DMA) {
-    // 3-slot ring: wait(tile j, tile j+1 may stay in flight) + barrier | DMA tile j+2 -> slot
-    // (j+2)%3, the slot tile j-1 was read from before that barrier | compute(slot j%3)
+    // double-buffered tiles: wait(tile j) + barrier | DMA tile j+1 -> buf (j+1)&1 | compute(buf j&1)
     tdma.init(ld);
-    dma_issue(0, 0);
-    if (ntiles > 1) dma_issue(1, 1);
+    dma_issue(0);
   } else {
     // double-buffered tiles: compute(buf j&1) | regs hold tile j+1 | store -> buf (j+1)&1 | ONE barrier
     load_tile<ROPE>(sk, Kb, ld, 0, T, cosT, sinT);
@@ -397,25 +393,14 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
       sv.load(Vb, ld, BN, T);
     }
   }
-  int slot = 0;  // j % NB
   for (int j = 0; j < ntiles; ++j) {
     const int k0 = j * BN;
-    const bf16_t* Kt = Ks + (DMA ? slot : (j & 1)) * (BN * HD);
-    const bf16_t* Vt = Vs + (DMA ? slot : (j & 1)) * (BN * HD);
+    const bf16_t* Kt = Ks + (j & 1) * (BN * HD);
+    const bf16_t* Vt = Vs + (j & 1) * (BN * HD);
     if constexpr (DMA) {
-      // per wave and tile: 2 x IPW DMA instructions (K and V); tile j+1's may stay outstanding
-      if (j + 1 < ntiles) {
-        constexpr int NV = 2 * TileDma<HD, BN>::IPW;
-        static_assert(NV == 2 || NV == 4 || NV == 8, "vmcnt immediate");
-        if constexpr (NV == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else if constexpr (NV == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (j + 2 < ntiles) dma_issue(j + 2, slot == 0 ? 2 : slot - 1);
-      slot = slot == 2 ? 0 : slot + 1;
+      if (j + 1 < ntiles) dma_issue(j + 1);
     }
     if (k0 <= q0w + 31) {  // else: whole tile above this wave's diagonal (wave-uniform)
       // K row fragments issued up front (V^T transposing reads stay next to their MFMAs: holding
