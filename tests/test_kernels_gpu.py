@@ -166,6 +166,8 @@ def _attn_ref(qkv, cos, sin, B, T, nh, nkv, hd):
 @pytest.mark.parametrize("B,T,nh,nkv,hd", [
     (2, 64, 2, 2, 64), (2, 200, 4, 4, 64), (1, 1024, 2, 2, 64), (2, 256, 4, 1, 64),
     (2, 130, 4, 4, 32), (1, 300, 2, 1, 128), (1, 2048, 1, 1, 64),
+    (8, 1024, 16, 16, 64),  # Llama-150M bench shape (batch 64 -> 8: same per-head work, smaller grid)
+    (4, 1024, 32, 4, 64),   # Llama-1B GQA 32/4
 ])
 def test_flash_attention_fwd_bwd(B, T, nh, nkv, hd):
     from nanodiloco_amd.ops.attention import rope_cache

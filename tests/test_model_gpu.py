@@ -40,6 +40,46 @@ def test_hip_vs_torch_model(kv):
     assert rel < 5e-2, rel
 
 
+def test_hip_vs_torch_loss_trajectory():
+    """40 clip + AdamW steps on learnable data (every sequence follows one fixed random next-token
+    permutation): the HIP bf16 model tracks the fp32 torch model's loss curve step by step, on fresh
+    batches (not a memorised one), GQA 4/2."""
+    V = 512
+    cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                                     num_key_value_heads=2, num_hidden_layers=2, vocab_size=V,
+                                     rms_norm_eps=1e-5))
+    perm = torch.randperm(V, generator=torch.Generator().manual_seed(0))
+
+    def batch(step):
+        tok = torch.randint(0, V, (8,), generator=torch.Generator().manual_seed(100 + step))
+        seq = [tok]
+        for _ in range(255):
+            seq.append(perm[seq[-1]])
+        return torch.stack(seq, 1).cuda()
+
+    curves = {}
+    for backend, dt in (("torch", torch.float32), ("hip", torch.bfloat16)):
+        ops.set_backend(backend)
+        m = LlamaForCausalLM(cfg, "cuda", dt).init_weights(3)
+        opt = FlatAdamW(m.store, lr=1.5e-3)
+        ls = []
+        for step in range(40):
+            ids = batch(step)
+            out = m(ids, labels=ids)
+            out.loss.backward()
+            opt.step()
+            m.store.zero_grad()
+            ls.append(out.loss.item())
+        curves[backend] = ls
+    t, h = curves["torch"], curves["hip"]
+    # 5-step means: single steps of a fast-learning run are chaotic in both precisions
+    wt = [sum(t[i:i + 5]) / 5 for i in range(0, 40, 5)]
+    wh = [sum(h[i:i + 5]) / 5 for i in range(0, 40, 5)]
+    curve = " ".join(f"{a:.3f}/{b:.3f}" for a, b in zip(t, h))
+    assert wt[-1] < 0.75 * t[0] and wh[-1] < 0.75 * h[0], curve
+    assert max(abs(a - b) for a, b in zip(wt, wh)) < 0.04 * t[0], curve
+
+
 def test_fp32_hip_path_runs():
     cfg = LlamaConfig.from_dict(dict(hidden_size=128, intermediate_size=256, num_attention_heads=4,
                                      num_hidden_layers=1, vocab_size=500, rms_norm_eps=1e-5))
