@@ -22,6 +22,8 @@ gradient, so ``dy`` is correct for any upstream value.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _ext
@@ -31,8 +33,13 @@ from .linear import library_gemm_fence, wgrad_accumulate
 IGNORE_INDEX = -100
 
 
-def _chunk_rows(V: int, elem: int, budget_bytes: int = 1 << 30) -> int:
-    return max(256, (budget_bytes // (V * elem)) // 256 * 256)
+# logits chunk budget (ND_CE_CHUNK_MB, default 4 GiB: a whole 64k-token micro-batch of a 32k
+# vocabulary in bf16 -- one GEMM triple per micro-batch; +0.35 % over 1 GiB chunks, profiles/r2_ce_chunk_ab.md)
+_CHUNK_BYTES = int(float(os.environ.get("ND_CE_CHUNK_MB", "4096")) * (1 << 20))
+
+
+def _chunk_rows(V: int, elem: int, budget_bytes: int = 0) -> int:
+    return max(256, ((budget_bytes or _CHUNK_BYTES) // (V * elem)) // 256 * 256)
 
 
 class LMHeadCEFn(torch.autograd.Function):
