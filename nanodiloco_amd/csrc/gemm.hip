@@ -858,7 +858,10 @@ __device__ __forceinline__ void mfma32f8z(const i32x8& a, const i32x8& b, f32x16
 }
 
 // FA / FB: formats of A (tokens) and B (weight); M, N in rows, K / lda / ldb in bf16 PAIRS (fp8 / 2)
-template <int FA, int FB, bool ILV>
+// LDM: 0 = LDS-DMA pieces ahead of each k-step-1 MFMA group, 1 = one DMA piece after each MFMA,
+// 2 = VGPR staging (buffer_load_dwordx4 one K-tile ahead into 64 VGPRs, ds_write_b128 between the
+// k-step-1 MFMAs, the next K-tile's loads issued right behind the writes)
+template <int FA, int FB, int LDM>
 __global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                           bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
                                                           int64_t ldb, int64_t ldc, const float* __restrict__ sa,
@@ -930,17 +933,51 @@ __global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restri
     for (int j = 0; j < 16; ++j) stage_piece(buf, j);
     advance();
   };
+  // LDM 2: piece j of the stream's current K-tile -> VGPRs, and VGPRs -> LDS (the DMA's lane-linear image)
+  auto load_piece = [&](int j) __attribute__((always_inline)) -> u32x4 {
+    const int h = (j >> 2) & 1, p = j & 3;
+    if (j < 8) return __builtin_amdgcn_raw_buffer_load_b128(make_rsrc(A + (int64_t)s_m0 * lda + (int64_t)s_kt * TK), va[h][p], 0, 0);
+    return __builtin_amdgcn_raw_buffer_load_b128(make_rsrc(B + (int64_t)s_n0 * ldb + (int64_t)s_kt * TK), vb[h][p], 0, 0);
+  };
+  auto write_piece = [&](int buf, int j, const u32x4& v) __attribute__((always_inline)) {
+    const int h = (j >> 2) & 1, p = j & 3;
+    char* d = reinterpret_cast<char*>(smem) + buf * BS * 2 + (j < 8 ? h : 2 + h) * HS * 2 + (w + 4 * p) * BLOCK_P + lane * 16;
+    *reinterpret_cast<u32x4*>(d) = v;
+  };
+  u32x4 stg[16];
+  auto ord = [](int k) __attribute__((always_inline)) { return (k & 1) * 8 + (k >> 1); };  // k-step-1 piece order
 
   f32x16 acc[4][4];  // written first by mfma32f8z
   if (total == 0) return;
   const int one = 0x7F7F7F7F;
 
+  if constexpr (LDM == 2) {
+    // pieces in the k-step-1 loop's order (0, 8, 1, 9, ...): the compiler's vmcnt bookkeeping
+    // then sees the same issue order on every path into the loop and can count exactly
+#pragma unroll
+    for (int k = 0; k < 16; ++k) stg[ord(k)] = load_piece(ord(k));
+    advance();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) write_piece(0, ord(k), stg[ord(k)]);
+    if (total > 1) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) stg[ord(k)] = load_piece(ord(k));
+      advance();
+#pragma unroll
+      for (int k = 0; k < 16; ++k) write_piece(1, ord(k), stg[ord(k)]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) stg[ord(k)] = load_piece(ord(k));
+    advance();
+    __builtin_amdgcn_s_waitcnt(LGKM0);
+  } else {
   stage_next(0);
   if (total > 1) {
     stage_next(1);
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   }
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -981,7 +1018,7 @@ __global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restri
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      if (more1) {
+      if (more1 && LDM != 2) {
         if (kt == 0 && lt > 0) {
           asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // K-tile g + 1 was issued before the 32 stores
         } else {
@@ -997,7 +1034,22 @@ __global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restri
       const bool stage_now = more2;
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        if constexpr (ILV) {
+        if constexpr (LDM == 2) {
+          // VGPR staging: K-tile g + 2 (loaded one K-tile ago) into the released buffer, and the
+          // same piece of K-tile g + 3 loaded right behind it
+          fb0[a] = frag8(bn, a * 32 + r32, kb);
+          fa0[a] = frag8(an, a * 32 + r32, kb);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            mfma32f8<FB, FA>(fb1[b], fa1[a], acc[a][b], one);
+            // unconditional (past the stream's end: rewrites a finished tile's pieces into a buffer
+            // nobody reads), so every path has the same VMEM issue order and hipcc's vmcnt waits
+            // stay exact (a conditional load made it drain to vmcnt(0) every K-tile)
+            const int j = (b & 1) * 8 + 2 * a + (b >> 1);
+            write_piece(buf, j, stg[j]);
+            stg[j] = load_piece(j);
+          }
+        } else if constexpr (LDM == 1) {
           // one LDS-DMA piece after each MFMA: a piece's issue stall overlaps the MFMA before it
           fb0[a] = frag8(bn, a * 32 + r32, kb);  // past the stream's end: reads unused LDS
           fa0[a] = frag8(an, a * 32 + r32, kb);
@@ -1020,7 +1072,7 @@ __global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restri
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (stage_now) advance();
+      if (LDM == 2 || stage_now) advance();
     }
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 7" ::: "memory");  // 16-pass MFMA results -> VALU
     const int c_tile = first + lt * G;
@@ -1166,29 +1218,33 @@ bool shapes_ok(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
 }
 int g_f8_variant = [] {
   const char* e = getenv("ND_GEMM_F8_VARIANT");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : -1;  // -1: auto (see launch_f8)
 }();
 
-template <int FA, int FB, bool ILV>
+template <int FA, int FB, int LDM>
 int launch_f8_v(const void* A, const void* B, void* C, int M, int N, int K2, int64_t lda2, int64_t ldb2, int64_t ldc,
               const float* sa, const float* sb, hipStream_t s) {
   const size_t lds = 2 * (size_t)(4 * HALF_P) * sizeof(bf16_t) + 4 * 16 * 68 * sizeof(float);  // 149 KiB
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm4_f8_kernel<FA, FB, ILV>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm4_f8_kernel<FA, FB, LDM>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return (int)attr;
   const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   const int grid = tiles < num_cus() ? tiles : num_cus();
-  hipLaunchKernelGGL((gemm4_f8_kernel<FA, FB, ILV>), dim3(grid), dim3(256), lds, s, (const bf16_t*)A, (const bf16_t*)B,
+  hipLaunchKernelGGL((gemm4_f8_kernel<FA, FB, LDM>), dim3(grid), dim3(256), lds, s, (const bf16_t*)A, (const bf16_t*)B,
                      (bf16_t*)C, M, N, K2, lda2, ldb2, ldc, sa, sb, g_group_m);
   ND_LAUNCH_CHECK();
 }
-// ND_GEMM_F8_VARIANT / nd_gemm_set_f8_variant: 1 (default) = one DMA piece per MFMA in k-step 1,
-// 0 = four pieces ahead of each group of four MFMAs
+// ND_GEMM_F8_VARIANT / nd_gemm_set_f8_variant: -1 (default) = auto by K, 1 = one DMA piece per MFMA
+// in k-step 1, 0 = four pieces ahead of each group of four MFMAs, 2 = VGPR-staged loads
 template <int FA, int FB>
 int launch_f8(const void* A, const void* B, void* C, int M, int N, int K2, int64_t lda2, int64_t ldb2, int64_t ldc,
               const float* sa, const float* sb, hipStream_t s) {
-  return g_f8_variant ? launch_f8_v<FA, FB, true>(A, B, C, M, N, K2, lda2, ldb2, ldc, sa, sb, s)
-                      : launch_f8_v<FA, FB, false>(A, B, C, M, N, K2, lda2, ldb2, ldc, sa, sb, s);
+  // auto: VGPR staging for long reductions (K > 4096 fp8: 0.81x vs 0.74x hipBLASLt at K = 5376), the
+  // interleaved DMA otherwise (its prologue and post-epilogue waits are shorter; profiles/r2_fp8_gemm_ab.md)
+  const int v = g_f8_variant >= 0 ? g_f8_variant : (K2 > 2048 ? 2 : 1);
+  if (v == 2) return launch_f8_v<FA, FB, 2>(A, B, C, M, N, K2, lda2, ldb2, ldc, sa, sb, s);
+  return v ? launch_f8_v<FA, FB, 1>(A, B, C, M, N, K2, lda2, ldb2, ldc, sa, sb, s)
+                      : launch_f8_v<FA, FB, 0>(A, B, C, M, N, K2, lda2, ldb2, ldc, sa, sb, s);
 }
 }  // namespace
 
@@ -1218,7 +1274,7 @@ ND_API int nd_gemm_set_variant(int v) {
 
 ND_API int nd_gemm_set_f8_variant(int v) {
   const int old = g_f8_variant;
-  if (v == 0 || v == 1) g_f8_variant = v;
+  if (v >= -1 && v <= 2) g_f8_variant = v;
   return old;
 }
 

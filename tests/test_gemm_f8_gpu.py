@@ -13,11 +13,16 @@ DEV = "cuda"
 E4, E5 = torch.float8_e4m3fn, torch.float8_e5m2
 
 
-@pytest.fixture(autouse=True)
-def _hip(hip_lib):
+@pytest.fixture(autouse=True, params=[-1, 0, 1, 2], ids=lambda v: f"ldm{v}")
+def _hip(hip_lib, request):
+    """Every loader variant of the kernel (csrc/gemm.hip g_f8_variant: DMA burst, DMA interleaved,
+    VGPR staging)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    old = G.set_gemm_f8_variant(request.param)
     torch.manual_seed(0)
+    yield
+    G.set_gemm_f8_variant(old)
 
 
 def q8(x, dt):
