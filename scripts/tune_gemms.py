@@ -5,6 +5,7 @@ nanodiloco_amd/tuning/tunableop_gfx950.csv (loaded at start-up by ops.tuned_gemm
 Runs forward + backward of each listed (model, micro-batch) configuration once with tuning on, so
 every projection / lm-head GEMM shape the trainer and bench.py issue is searched.  One GPU, a few
 minutes.  Usage:  python scripts/tune_gemms.py [llama_150m.json:32 llama_150m.json:8 ...]
+(FP8=1: build the models with --fp8 projections, so the hipBLASLt fp8 GEMMs are tuned too.)
 """
 import os
 import sys
@@ -33,7 +34,8 @@ def main():
         name, mb = spec.split(":")
         cfg = resolve_llama_config(name)
         t0 = time.time()
-        m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16).init_weights(0)
+        fp8 = os.environ.get("FP8", "0") == "1"  # also tune the fp8 projections' _scaled_mm (ScaledGemm)
+        m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16, fp8=fp8).init_weights(0)
         ids = torch.randint(0, cfg.vocab_size, (int(mb), seq), device="cuda")
         o = m(ids, labels=ids)
         o.loss.backward()
