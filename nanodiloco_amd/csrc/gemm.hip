@@ -844,6 +844,13 @@ __device__ __forceinline__ void mfma32f8(const i32x8& a, const i32x8& b, f32x16&
     asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:1 blgp:1" : "+a"(c) : "v"(a), "v"(b), "v"(one));
 }
 
+// 16-B buffer load the compiler does not track (LDM 3): the caller waits with an explicit vmcnt
+__device__ __forceinline__ u32x4 bload_untracked(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  u32x4 v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
+  return v;
+}
+
 // the same with a zero accumulator input (first k-step of a tile): no per-tile AGPR zeroing
 template <int CB, int BL>
 __device__ __forceinline__ void mfma32f8z(const i32x8& a, const i32x8& b, f32x16& c, int one) {
@@ -936,6 +943,10 @@ __global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restri
   // LDM 2: piece j of the stream's current K-tile -> VGPRs, and VGPRs -> LDS (the DMA's lane-linear image)
   auto load_piece = [&](int j) __attribute__((always_inline)) -> u32x4 {
     const int h = (j >> 2) & 1, p = j & 3;
+    if constexpr (LDM == 3) {
+      if (j < 8) return bload_untracked(make_rsrc(A + (int64_t)s_m0 * lda + (int64_t)s_kt * TK), va[h][p]);
+      return bload_untracked(make_rsrc(B + (int64_t)s_n0 * ldb + (int64_t)s_kt * TK), vb[h][p]);
+    }
     if (j < 8) return __builtin_amdgcn_raw_buffer_load_b128(make_rsrc(A + (int64_t)s_m0 * lda + (int64_t)s_kt * TK), va[h][p], 0, 0);
     return __builtin_amdgcn_raw_buffer_load_b128(make_rsrc(B + (int64_t)s_n0 * ldb + (int64_t)s_kt * TK), vb[h][p], 0, 0);
   };
@@ -951,18 +962,20 @@ __global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restri
   if (total == 0) return;
   const int one = 0x7F7F7F7F;
 
-  if constexpr (LDM == 2) {
+  if constexpr (LDM >= 2) {
     // pieces in the k-step-1 loop's order (0, 8, 1, 9, ...): the compiler's vmcnt bookkeeping
     // then sees the same issue order on every path into the loop and can count exactly
 #pragma unroll
     for (int k = 0; k < 16; ++k) stg[ord(k)] = load_piece(ord(k));
     advance();
+    if constexpr (LDM == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int k = 0; k < 16; ++k) write_piece(0, ord(k), stg[ord(k)]);
     if (total > 1) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) stg[ord(k)] = load_piece(ord(k));
       advance();
+      if constexpr (LDM == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
       for (int k = 0; k < 16; ++k) write_piece(1, ord(k), stg[ord(k)]);
     }
@@ -1018,7 +1031,7 @@ __global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restri
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      if (more1 && LDM != 2) {
+      if (more1 && LDM < 2) {
         if (kt == 0 && lt > 0) {
           asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // K-tile g + 1 was issued before the 32 stores
         } else {
@@ -1034,7 +1047,7 @@ __global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restri
       const bool stage_now = more2;
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        if constexpr (LDM == 2) {
+        if constexpr (LDM >= 2) {
           // VGPR staging: K-tile g + 2 (loaded one K-tile ago) into the released buffer, and the
           // same piece of K-tile g + 3 loaded right behind it
           fb0[a] = frag8(bn, a * 32 + r32, kb);
@@ -1046,6 +1059,12 @@ __global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restri
             // nobody reads), so every path has the same VMEM issue order and hipcc's vmcnt waits
             // stay exact (a conditional load made it drain to vmcnt(0) every K-tile)
             const int j = (b & 1) * 8 + 2 * a + (b >> 1);
+            if constexpr (LDM == 3) {
+              // untracked loads: each piece's load is the 16th-newest VMEM op (plus the tile's 32
+              // stores right after an epilogue, which stay in flight)
+              if (kt == 0 && lt > 0) asm volatile("s_waitcnt vmcnt(47)" ::: "memory");
+              else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+            }
             write_piece(buf, j, stg[j]);
             stg[j] = load_piece(j);
           }
@@ -1072,7 +1091,7 @@ __global__ void __launch_bounds__(256, 1) gemm4_f8_kernel(const bf16_t* __restri
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (LDM == 2 || stage_now) advance();
+      if (LDM >= 2 || stage_now) advance();
     }
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 7" ::: "memory");  // 16-pass MFMA results -> VALU
     const int c_tile = first + lt * G;
@@ -1243,6 +1262,7 @@ int launch_f8(const void* A, const void* B, void* C, int M, int N, int K2, int64
   // interleaved DMA otherwise (its prologue and post-epilogue waits are shorter; profiles/r2_fp8_gemm_ab.md)
   const int v = g_f8_variant >= 0 ? g_f8_variant : (K2 > 2048 ? 2 : 1);
   if (v == 2) return launch_f8_v<FA, FB, 2>(A, B, C, M, N, K2, lda2, ldb2, ldc, sa, sb, s);
+  if (v == 3) return launch_f8_v<FA, FB, 3>(A, B, C, M, N, K2, lda2, ldb2, ldc, sa, sb, s);
   return v ? launch_f8_v<FA, FB, 1>(A, B, C, M, N, K2, lda2, ldb2, ldc, sa, sb, s)
                       : launch_f8_v<FA, FB, 0>(A, B, C, M, N, K2, lda2, ldb2, ldc, sa, sb, s);
 }
@@ -1274,7 +1294,7 @@ ND_API int nd_gemm_set_variant(int v) {
 
 ND_API int nd_gemm_set_f8_variant(int v) {
   const int old = g_f8_variant;
-  if (v >= -1 && v <= 2) g_f8_variant = v;
+  if (v >= -1 && v <= 3) g_f8_variant = v;
   return old;
 }
 

@@ -6,7 +6,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 600 python -u -m pytest tests/test_gemm_f8_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r2f8/pytest.log 2>&1; rc=$?
 tail -3 gpurun_out/r2f8/pytest.log
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python scripts/gemm_nt_bench.py --fp8 --variants 1:4,2:4 --rounds 5 > gpurun_out/r2f8/ab8.log 2>&1 || exit $?
+timeout -k 10 300 python scripts/gemm_nt_bench.py --fp8 --variants 1:4,2:4,3:4 --rounds 5 > gpurun_out/r2f8/ab8.log 2>&1 || exit $?
 cat gpurun_out/r2f8/ab8.log
 if [ -n "$E2E" ]; then
 for i in 1 2; do

@@ -13,7 +13,7 @@ DEV = "cuda"
 E4, E5 = torch.float8_e4m3fn, torch.float8_e5m2
 
 
-@pytest.fixture(autouse=True, params=[-1, 0, 1, 2], ids=lambda v: f"ldm{v}")
+@pytest.fixture(autouse=True, params=[-1, 0, 1, 2, 3], ids=lambda v: f"ldm{v}")
 def _hip(hip_lib, request):
     """Every loader variant of the kernel (csrc/gemm.hip g_f8_variant: DMA burst, DMA interleaved,
     VGPR staging)."""
