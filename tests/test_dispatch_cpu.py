@@ -1,0 +1,51 @@
+"""CPU checks of the op-dispatch switches added in round 2: fp8 GEMM backend selection, the own
+fp8 GEMM's shape gate, and the lm-head chunking rule (one chunk per 64k-token micro-batch)."""
+import pytest
+import torch
+
+from nanodiloco_amd.ops import cross_entropy as ce
+from nanodiloco_amd.ops import fp8
+from nanodiloco_amd.ops import gemm as G
+
+
+def test_fp8_gemm_backend_switch():
+    old = fp8.fp8_gemm_backend()
+    assert old == "hipblaslt"  # measured default (profiles/r2_fp8_gemm_ab.md)
+    try:
+        fp8.set_fp8_gemm("hip")
+        assert fp8.fp8_gemm_backend() == "hip"
+        with pytest.raises(ValueError):
+            fp8.set_fp8_gemm("cublas")
+    finally:
+        fp8.set_fp8_gemm(old)
+
+
+def test_f8_nt_supported_gate_on_cpu_and_shapes():
+    a = torch.zeros(64, 256, dtype=torch.float8_e4m3fn)
+    assert not G.f8_nt_supported(a, a)  # CPU tensors never take the HIP kernel
+    assert not G.f8_nt_supported(a.float(), a.float())
+
+
+def test_lm_head_chunk_rows():
+    # 4 GiB budget: a whole 65,536-row micro-batch of a 32k vocabulary in bf16 is one chunk
+    assert ce._chunk_rows(32000, 2) >= 65536
+    assert ce._chunk_rows(32000, 2) % 256 == 0
+    assert ce._chunk_rows(32000, 2, budget_bytes=1 << 30) == 16640  # (4 equal chunks of 16384 in the forward)
+    assert ce._chunk_rows(10 ** 9, 4) == 256  # never below one 256-row block
+
+
+def test_lm_head_ce_chunked_matches_unchunked():
+    torch.manual_seed(0)
+    n, d, V = 600, 32, 50
+    y = torch.randn(n, d, requires_grad=True)
+    w = torch.randn(V, d) * 0.1
+    t = torch.randint(0, V, (n,))
+    t[::7] = ce.IGNORE_INDEX
+    gw1, gw2 = torch.zeros(V, d), torch.zeros(V, d)
+    l1 = ce.lm_head_ce(y, w, gw1, t, chunk_rows=256)
+    (g1,) = torch.autograd.grad(l1, y)
+    l2 = ce.lm_head_ce(y, w, gw2, t)
+    (g2,) = torch.autograd.grad(l2, y)
+    assert torch.allclose(l1, l2, atol=1e-5)
+    assert torch.allclose(g1, g2, atol=1e-6)
+    assert torch.allclose(gw1, gw2, atol=1e-5)
