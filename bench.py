@@ -28,14 +28,9 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from nanodiloco_amd import ops  # noqa: E402
-from nanodiloco_amd.config import resolve_llama_config  # noqa: E402
-from nanodiloco_amd.data import SyntheticTokens  # noqa: E402
-from nanodiloco_amd.models import LlamaForCausalLM  # noqa: E402
-from nanodiloco_amd.optim import FlatAdamW, FlatOuterNesterov  # noqa: E402
-from nanodiloco_amd.parallel.diloco import Diloco  # noqa: E402
 from nanodiloco_amd.ops.tuned_gemm import enable_tuned_gemms  # noqa: E402
-from nanodiloco_amd.parallel.dist import barrier, init_distributed  # noqa: E402
-from nanodiloco_amd.parallel.inner_ddp import InnerGradSync  # noqa: E402
+from nanodiloco_amd.parallel.dist import barrier  # noqa: E402
+from nanodiloco_amd.trainer import TrainArgs, Trainer  # noqa: E402
 
 BASELINE_TOKENS_PER_S = None  # the reference publishes no number
 METRIC = "tokens/sec (whole node) Llama-150M, 8 DiLoCo workers H=100; bytes/outer-step"  # BASELINE.json
@@ -50,14 +45,17 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="llama_150m.json")
     ap.add_argument("--batch-size", type=int, default=256, help="sequences per worker per inner step (reference)")
-    ap.add_argument("--micro-batch", type=int, default=64,
-                    help="sequences per forward/backward (64: best of 16/32/64/128/256 on MI355X, same global batch)")
+    ap.add_argument("--micro-batch", default="auto",
+                    help="sequences per forward/backward; auto = the trainer's --per-device-batch-size auto "
+                         "(64 for Llama-150M: best of 16/32/64/128/256 on MI355X, same global batch)")
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--inner-steps", type=int, default=100)
     ap.add_argument("--inner-dp", type=int, default=1)
     ap.add_argument("--ops", default="auto", choices=["auto", "hip", "torch"])
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
-                    help="collective backend (auto = nccl/RCCL on GPU); gloo lets several ranks share one GPU")
+                    help="collective backend (auto = nccl/RCCL on GPU); gloo lets several ranks share one GPU. "
+                         "An explicit backend at world size 1 still creates a one-rank process group and "
+                         "issues every collective (the RCCL path on one GPU)")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--bucket-mb", type=float, default=128.0)
     ap.add_argument("--overlap-outer", action="store_true")
@@ -88,8 +86,7 @@ def parse():
 
 def main():
     a = parse()
-    ops.set_backend(a.ops)
-    ops.set_wgrad_overlap(a.wgrad_overlap)
+    # kernel-path switches the trainer does not own (A/B flags); set before the model is built
     ops.set_fused_swiglu(bool(a.fused_swiglu))
     ops.set_dgrad_transposed(bool(a.dgrad_t))
     ops.set_attn_fused_stats(bool(a.attn_fused_stats))
@@ -99,55 +96,35 @@ def main():
         _fp8.set_fp8_gemm(a.fp8_gemm)
     if a.wgrad_variant:
         os.environ["ND_WGRAD_VARIANT"] = a.wgrad_variant
-    env = init_distributed(a.backend, a.inner_dp)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    H = a.inner_steps
+    # the product's training step: Trainer.inner_step (micro-batch fwd+bwd, inner-DDP sync, clip +
+    # AdamW) and Diloco.outer_step, exactly what `python -m nanodiloco_amd` runs
+    targs = TrainArgs(
+        seed=1337, batch_size=a.batch_size, per_device_batch_size=a.micro_batch, seq_length=a.seq_len,
+        warmup_steps=100, total_steps=H * max(1, -(-10_000 // H)), inner_steps=H, lr=4e-4, outer_lr=0.7,
+        llama_config_file=a.model, data="synthetic", ops=a.ops, backend=a.backend, inner_dp=a.inner_dp,
+        comm_dtype=a.comm_dtype, bucket_mb=a.bucket_mb, overlap_outer=a.overlap_outer, fp8=a.fp8,
+        fp8_wgrad=a.fp8_wgrad, tuned_gemm=not a.no_tuned_gemm and not a.tuned_gemm_file,
+        hip_graph="on" if a.hip_graph else "off", wgrad_overlap=bool(a.wgrad_overlap), log_every=0, wandb="off",
+        phase_timing=False, force_collectives=a.backend != "auto" and world == 1)
+    tr = Trainer(targs)
+    env, cfg, dl = tr.env, tr.llama_config, tr.diloco
+    ops.set_wgrad_overlap(a.wgrad_overlap)  # mode 2 (unfenced A/B) is not a trainer option
     if env.world_size != a.gpus and env.rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
-    if env.device.type == "cuda" and not a.no_tuned_gemm:
-        if a.tuned_gemm_file:
-            enable_tuned_gemms(env.device, a.tuned_gemm_file)
-        else:
-            enable_tuned_gemms(env.device)
-    cfg = resolve_llama_config(a.model)
-    dtype = torch.bfloat16 if env.device.type == "cuda" else torch.float32
-    model = LlamaForCausalLM(cfg, env.device, dtype, fp8=a.fp8, fp8_wgrad=a.fp8_wgrad).init_weights(1337)
-    inner = FlatAdamW(model.store, lr=4e-4)
-    outer = FlatOuterNesterov(model.store, lr=0.7, momentum=0.9)
-    comm_dtype = torch.bfloat16 if a.comm_dtype == "bf16" else torch.float32
-    total = 10_000
-    dl = Diloco(model, inner, outer, warmup_steps=100, total_steps=total, inner_steps=a.inner_steps, env=env,
-                comm_dtype=comm_dtype, bucket_mb=a.bucket_mb, overlap=a.overlap_outer)
-    isync = InnerGradSync(model, dl.inner_comm)
-    accum = a.batch_size // a.micro_batch
-    data = SyntheticTokens(cfg.vocab_size, a.seq_len, a.micro_batch, seed=1337, rank=env.rank, device=env.device)
-    loss_scale = 1.0 / accum / env.inner_dp
-    model.train()
+    if env.device.type == "cuda" and a.tuned_gemm_file:
+        enable_tuned_gemms(env.device, a.tuned_gemm_file)
+    micro = targs.per_device_batch_size  # resolved by the trainer
+    accum = tr.grad_accum
+    tr.model.train()
     state = {"step": 0}
 
-    graphed = None
-    if a.hip_graph:
-        if env.inner_dp > 1:
-            raise SystemExit("--hip-graph needs --inner-dp 1")
-        from nanodiloco_amd.utils.graphs import GraphedMicroStep
-        graphed = GraphedMicroStep(model)
-
     def inner_step():
-        loss = None
-        for m in range(accum):
-            b = next(data)
-            if m == accum - 1:
-                isync.arm()
-            if graphed is not None:
-                l_m = graphed(b["input_ids"], b["labels"], loss_scale)
-            else:
-                out = model(b["input_ids"], labels=b["labels"], loss_scale=loss_scale)
-                out.loss.backward()
-                l_m = out.loss.detach()
-            loss = l_m.clone() if loss is None else loss + l_m
-        isync.finish()
-        dl.inner_step()
+        loss = tr.inner_step()
         state["step"] += 1
         outer_done = False
-        if state["step"] % a.inner_steps == 0:
+        if state["step"] % H == 0:
             dl.outer_step()
             outer_done = True
         return loss, outer_done
@@ -179,13 +156,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     outer_ms = dl.comm_ms()  # device time of the last outer step (HIP events; after the timed window)
+    # one more outer step, untimed and serialized, split into pseudo-gradient / all-reduce / update
+    phases = {}
+    if not a.overlap_outer and env.device.type == "cuda":
+        dl.outer_step(phases=True)
+        phases = dl.outer_phase_ms()
+    vals = [outer_ms] + [phases.get(k, 0.0) for k in ("pseudograd_ms", "allreduce_ms", "outer_update_ms")]
     if env.is_distributed:
-        t = torch.tensor([outer_ms], dtype=torch.float64, device=env.device)
+        t = torch.tensor(vals, dtype=torch.float64, device=env.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        outer_ms = float(t.item())
+        vals = t.tolist()
+    outer_ms = vals[0]
     tokens = a.batch_size * a.seq_len * a.steps * env.world_size
     tps = tokens / elapsed
-    final_loss = float((loss / accum).item()) if loss is not None else float("nan")
+    final_loss = float(loss.item()) if loss is not None else float("nan")
     if a.profile_steps and env.rank == 0:
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
@@ -196,6 +180,7 @@ def main():
     if env.rank == 0:
         model_name = MODEL_NAMES.get(os.path.splitext(os.path.basename(a.model))[0], a.model)
         mfu_flops = cfg.flops_per_token(a.seq_len) * tps / max(1, env.world_size)
+        comm_dtype = torch.bfloat16 if a.comm_dtype == "bf16" else torch.float32
         out = {
             "metric": METRIC if model_name == "Llama-150M" else
             f"tokens/sec (whole node) {model_name}, DiLoCo workers H={a.inner_steps}",
@@ -208,7 +193,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (tps / BASELINE_TOKENS_PER_S) if BASELINE_TOKENS_PER_S else None,
-            "dtype": ("fp8" if a.fp8 else "bf16") if dtype == torch.bfloat16 else "fp32",
+            "dtype": ("fp8" if a.fp8 else "bf16") if tr.compute_dtype == torch.bfloat16 else "fp32",
             "data": "synthetic",
             "config": {
                 "model": model_name,
@@ -216,16 +201,21 @@ def main():
                 "seq_len": a.seq_len,
                 "parallelism": f"diloco{env.num_workers}" + (f"x_ddp{env.inner_dp}" if env.inner_dp > 1 else ""),
                 "per_worker_batch": a.batch_size,
-                "micro_batch": a.micro_batch,
+                "micro_batch": micro,
+                "grad_accum": accum,
                 "inner_steps_H": a.inner_steps,
                 "params": cfg.num_params(),
             },
-            "bytes_per_outer_step": dl.bytes_per_outer_step if env.num_workers > 1 else model.store.numel * (
+            "step_driver": "Trainer.inner_step",
+            "bytes_per_outer_step": dl.bytes_per_outer_step if dl.outer_comm.enabled else tr.model.store.numel * (
                 2 if comm_dtype == torch.bfloat16 else 4),
             "outer_steps_in_window": n_outer,
             # outer-step cost as seen by the compute stream (HIP events: pseudo-gradient + bucketed
             # RCCL all-reduce + fused Nesterov), host wall time per outer step, and calls per outer step
             "outer_step_ms": round(outer_ms, 3),
+            # the same step serialized, per phase (untimed, after the window): what RCCL costs per N
+            "outer_phase_ms": {k: round(v, 3) for k, v in
+                               zip(("pseudograd", "allreduce", "outer_update"), vals[1:])} if phases else None,
             "outer_step_wall_ms": round(1000.0 * dl.avg_sync_time, 3),
             "allreduce_calls_per_outer_step": dl.buckets_per_outer_step,
             "comm_backend": env.backend,

@@ -641,6 +641,17 @@ static int plan(int M, int N, int K, int* S_out) {
   return 0;
 }
 
+// K range per split, rounded up to whole bk tiles; S shrinks until every split owns at least one
+// tile (with the rounding, the last split could otherwise be empty -- e.g. K = 41 * 64, S = 8 -- and
+// its slab plane would never be written while slab_reduce_kernel still sums all S planes)
+static int fit_kchunk(int K, int* S, int bk) {
+  for (;;) {
+    const int kchunk = ((K + *S - 1) / *S + bk - 1) / bk * bk;
+    if (*S <= 1 || (int64_t)(*S - 1) * kchunk < K) return kchunk;
+    --*S;
+  }
+}
+
 // Number of K splits for this shape (slab workspace = S * M * N floats when S > 1).
 ND_API int nd_wgrad_splits(int M, int N, int K) {
   int S;
@@ -667,7 +678,7 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
   // 4-13 % SLOWER per kernel than the compiler's own schedule at 32k and 64k tokens, -1.7 % e2e
   const bool sched = ev && ev[0] == 'd' && ev[3] == 's';
   if (large && variant == 5 && M >= 8 && N >= 8 && K % BK3 == 0) {  // "4w": 4-wave, AGPR-pinned accumulators
-    const int kchunk = ((K + S - 1) / S + BK3 - 1) / BK3 * BK3;
+    const int kchunk = fit_kchunk(K, &S, BK3);
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB
     static const hipError_t attr4 = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad4_kernel),
@@ -676,7 +687,7 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
     hipLaunchKernelGGL(wgrad4_kernel, dim3(tiles * S), dim3(256), lds, s, (const bf16_t*)A, (const bf16_t*)B, C, slab,
                        M, N, K, lda, ldb, ldc, S, kchunk);
   } else if (large && variant == 4) {  // "nodma": compute-only diagnostic
-    const int kchunk = ((K + S - 1) / S + BK3 - 1) / BK3 * BK3;
+    const int kchunk = fit_kchunk(K, &S, BK3);
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);
     static const hipError_t attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_dma_kernel<true, true>),
@@ -685,7 +696,7 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
     hipLaunchKernelGGL((wgrad_dma_kernel<true, true>), dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A,
                        (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
   } else if (large && variant != 1 && M >= 8 && N >= 8) {
-    const int kchunk = ((K + S - 1) / S + BK3 - 1) / BK3 * BK3;
+    const int kchunk = fit_kchunk(K, &S, BK3);
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB
     static const hipError_t attr_ok =
@@ -701,13 +712,13 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
       hipLaunchKernelGGL(wgrad_dma_kernel<false>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A,
                          (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
   } else if (large) {
-    const int kchunk = ((K + S - 1) / S + BK2 - 1) / BK2 * BK2;
+    const int kchunk = fit_kchunk(K, &S, BK2);
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK2 * (BM2 + BN2) * sizeof(bf16_t);
     hipLaunchKernelGGL(wgrad256_kernel, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B, C,
                        slab, M, N, K, lda, ldb, ldc, S, kchunk);
   } else {
-    const int kchunk = ((K + S - 1) / S + BK - 1) / BK * BK;
+    const int kchunk = fit_kchunk(K, &S, BK);
     const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * S), dim3(256), 0, s, (const bf16_t*)A, (const bf16_t*)B, C, slab, M,
                        N, K, lda, ldb, ldc, S, kchunk);

@@ -48,6 +48,12 @@ def make_collate(tokenizer, seq_length: int, mask_pad_labels: bool = True):
         padded = tokenizer.pad(batch, padding="longest", max_length=seq_length, pad_to_multiple_of=8,
                                return_tensors="pt")
         labels = padded["input_ids"].clone()
+        if "attention_mask" in padded:
+            # the attention kernels take one key start per sequence (left / right padding only): a mask
+            # with a hole would silently attend with the wrong mask, so reject it here, on the host copy
+            # (no device sync)
+            from ..ops.attention import check_padding
+            check_padding(padded["attention_mask"])
         if mask_pad_labels and "attention_mask" in padded:
             labels[padded["attention_mask"] == 0] = -100
         padded["labels"] = labels

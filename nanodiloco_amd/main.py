@@ -18,6 +18,11 @@ from .trainer import TrainArgs, Trainer
 
 
 TRISTATE = {"hip_graph"}  # on | off | auto; the bare flag means "on"
+AUTO_INT = {"per_device_batch_size"}  # an int or "auto"
+
+
+def _int_or_auto(s: str):
+    return "auto" if s.lower() == "auto" else int(s)
 
 
 def _bool(s: str) -> bool:
@@ -29,7 +34,9 @@ def build_parser() -> argparse.ArgumentParser:
     for f in dataclasses.fields(TrainArgs):
         flag = "--" + f.name.replace("_", "-")
         default = f.default
-        if f.type in (bool, "bool"):
+        if f.name in AUTO_INT:
+            p.add_argument(flag, type=_int_or_auto, default=default)
+        elif f.type in (bool, "bool"):
             p.add_argument(flag, type=_bool, nargs="?", const=True, default=default)
         elif f.type in (int, "int"):
             p.add_argument(flag, type=int, default=default)

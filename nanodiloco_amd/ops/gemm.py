@@ -11,9 +11,11 @@
                      as they lie in memory and fragments formed with transposing LDS reads, with a
                      deterministic split-K for the small outputs.
 
-``set_gemm_backend("blas")`` routes the NT GEMMs back to hipBLASLt (``torch.mm``) for A/B runs; the
-default on a GPU is our kernels.  Shapes outside ``nt_supported`` (K % 64, N % 4, alignment) use
-hipBLASLt.
+Where each kernel runs: ``wgrad`` is the weight gradient of every projection on the default path
+(ops/linear.py).  The NT kernels are called by ``ops.linear`` / ``ops.cross_entropy`` only when
+their switches select them (``ops.linear.set_own_gemm`` and the fused-epilogue switches, see
+ops/linear.py); ``set_gemm_backend("blas")`` disables them for A/B runs.  Shapes outside
+``nt_supported`` (K % 64, N % 4, alignment) always use hipBLASLt (``torch.mm``).
 """
 from __future__ import annotations
 

@@ -70,11 +70,13 @@ class PendingAllReduce:
 class FlatCommunicator:
     """Bucketed async all-reduce / broadcast / all-gather on flat buffers for one process group."""
 
-    def __init__(self, group, group_size: int, bucket_mb: float = 128.0, enabled: bool = True):
+    def __init__(self, group, group_size: int, bucket_mb: float = 128.0, enabled: bool = True, force: bool = False):
+        """``force``: issue the collectives even for a one-member group (a one-rank process group from
+        ``init_distributed(force_pg=True)``), so the communicator path runs on a single GPU."""
         self.group = group
         self.size = group_size
         self.bucket_bytes = int(bucket_mb * (1 << 20))
-        self.enabled = enabled and group_size > 1
+        self.enabled = enabled and (group_size > 1 or force)
         self.stats = CommStats()
 
     def all_reduce_async(self, flat: torch.Tensor, ranges: Optional[Sequence[Range]] = None) -> PendingAllReduce:

@@ -68,9 +68,10 @@ class Diloco:
         self.offload_snapshot = offload_snapshot
         self.debug_checks = debug_checks
         e = self.env
-        self.outer_comm = FlatCommunicator(e.outer_group, e.num_workers, bucket_mb)
-        self.inner_comm = FlatCommunicator(e.inner_group, e.inner_dp, bucket_mb)
-        self.world_comm = FlatCommunicator(e.world_group, e.world_size, bucket_mb)
+        f = e.force_collectives
+        self.outer_comm = FlatCommunicator(e.outer_group, e.num_workers, bucket_mb, force=f)
+        self.inner_comm = FlatCommunicator(e.inner_group, e.inner_dp, bucket_mb, force=f)
+        self.world_comm = FlatCommunicator(e.world_group, e.world_size, bucket_mb, force=f)
         n = self.store.numel
         # shard of the flat vector this GPU reduces over the outer group (two-level mode)
         k = e.inner_dp
@@ -118,7 +119,7 @@ class Diloco:
     def bytes_per_outer_step(self) -> int:
         """Pseudo-gradient payload each GPU contributes to the outer all-reduce."""
         a, b = self.my_shard
-        return (b - a) * torch.tensor([], dtype=self.comm_dtype).element_size() if self.env.num_workers > 1 else 0
+        return (b - a) * torch.tensor([], dtype=self.comm_dtype).element_size() if self.outer_comm.enabled else 0
 
     def comm_ms(self) -> float:
         """Device time of the last outer step (HIP events on the compute stream, from the pseudo-
@@ -133,7 +134,7 @@ class Diloco:
     @property
     def buckets_per_outer_step(self) -> int:
         """Number of all-reduce calls one outer step issues (the reference issues one per tensor)."""
-        if self.env.num_workers <= 1:
+        if not self.outer_comm.enabled:
             return 0
         a, b = self.my_shard
         return len(plan_buckets(0, b - a, self.delta.element_size(), self.outer_comm.bucket_bytes))
@@ -157,7 +158,11 @@ class Diloco:
             self.check_inner_replicas()
 
     # ------------------------------------------------------------------ outer step
-    def outer_step(self):
+    def outer_step(self, phases: bool = False):
+        """One outer step.  ``phases=True`` (diagnostics, e.g. bench.py after its timed window) runs it
+        serialized -- every bucket's all-reduce completes before the first Nesterov update -- and
+        records HIP events between the phases, so :meth:`outer_phase_ms` can split the step into
+        pseudo-gradient / collective / outer-update time; the default pipelines buckets instead."""
         t0 = time.perf_counter()
         cuda = self.store.device.type == "cuda"
         ev0 = torch.cuda.Event(enable_timing=True) if cuda else None
@@ -174,13 +179,35 @@ class Diloco:
                 self.drift_base.copy_(self.delta)
             else:
                 ops.pseudograd(sync[a:b], master[a:b], self.drift_base)
+        marks = None
+        if phases and cuda and not self.overlap:
+            marks = [ev0, torch.cuda.Event(enable_timing=True)]
+            marks[1].record()
         pend = self.outer_comm.all_reduce_async(self.delta)
+        if marks is not None:
+            pend.wait_all()  # serialized: the compute stream waits for every bucket here
+            marks.append(torch.cuda.Event(enable_timing=True))
+            marks[2].record()
         self._pending = (pend, sync, ev0, t0)
         self.outer_step_count += 1
         if not self.overlap:
             self._finish_outer()
+            if marks is not None:
+                marks.append(self._comm_events[-1][1])
+                self._phase_marks = marks
         else:
             self._sync_time += time.perf_counter() - t0
+
+    def outer_phase_ms(self) -> dict:
+        """Device time of the last ``outer_step(phases=True)``: pseudo-gradient kernel, bucketed
+        all-reduce (from the compute stream's view: issue to last bucket done), outer Nesterov update
+        (+ the two-level all-gathers).  Empty if no phased step ran."""
+        m = getattr(self, "_phase_marks", None)
+        if not m:
+            return {}
+        m[-1].synchronize()
+        return {"pseudograd_ms": m[0].elapsed_time(m[1]), "allreduce_ms": m[1].elapsed_time(m[2]),
+                "outer_update_ms": m[2].elapsed_time(m[3])}
 
     def _finish_outer(self):
         pend, sync, ev0, t0 = self._pending

@@ -7,6 +7,9 @@ Here:
 * backend ``auto`` = ``nccl`` (RCCL over xGMI on MI355X) when GPUs exist, else ``gloo`` (fixes the
   reference's hard-coded NCCL, SURVEY.md Q8 -- BASELINE config 1 runs on CPU/gloo);
 * world size 1 without torchrun works with no process group at all (collectives become no-ops);
+  ``force_pg=True`` creates a one-rank process group anyway (in-memory store, no rendezvous) and
+  keeps every collective call live, so the RCCL path -- communicator init, bucketed async
+  all-reduce, broadcast, sub-group all-gather, device barrier -- runs on a one-GPU box too;
 * ``inner_dp = K`` splits the world into W/K DiLoCo workers of K GPUs each (BASELINE config 3).
   Inner groups are blocks of K consecutive ranks (xGMI neighbours on one node); outer groups are
   the ranks with the same index inside their inner group, so an outer all-reduce of shard r only
@@ -34,13 +37,14 @@ class DistEnv:
     inner_rank: int = 0
     worker: int = 0           # DiLoCo worker index  (rank // inner_dp)
     num_workers: int = 1      # world_size // inner_dp
+    force_collectives: bool = False  # world size 1 with a live process group (force_pg)
     inner_group: Optional[object] = None
     outer_group: Optional[object] = None
     world_group: Optional[object] = None
 
     @property
     def is_distributed(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.force_collectives
 
     @property
     def is_main(self) -> bool:
@@ -53,7 +57,7 @@ def _env_int(k, d):
 
 
 def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[str] = None,
-                     timeout_s: float = 1800.0) -> DistEnv:
+                     timeout_s: float = 1800.0, force_pg: bool = False) -> DistEnv:
     rank = _env_int("RANK", 0)
     world = _env_int("WORLD_SIZE", 1)
     local_rank = _env_int("LOCAL_RANK", 0)
@@ -72,7 +76,7 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
     env = DistEnv(rank=rank, world_size=world, local_rank=local_rank, device=dev, backend="none",
                   inner_dp=inner_dp, inner_rank=rank % inner_dp, worker=rank // inner_dp,
                   num_workers=world // inner_dp)
-    if world == 1:
+    if world == 1 and not force_pg:
         return env
     # failure detection: a hung / failed collective surfaces as an error on every rank (instead of a
     # silent hang) after `timeout_s`; torchrun --max-restarts + --resume then restart from the last
@@ -82,8 +86,11 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = dev  # eager RCCL communicator init
+        if world == 1 and "MASTER_ADDR" not in os.environ:
+            kw.update(store=dist.HashStore(), rank=0, world_size=1)  # one rank: nothing to rendezvous with
         dist.init_process_group(**kw)
     env.backend = backend
+    env.force_collectives = world == 1
     env.world_group = dist.group.WORLD
     if inner_dp == 1:
         env.inner_group = None

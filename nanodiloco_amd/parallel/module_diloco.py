@@ -69,7 +69,11 @@ class _Group:
 
     @torch.no_grad()
     def take_snapshot(self):
-        self.snapshot.copy_(self.gather(), non_blocking=True)
+        # a device -> pinned-host copy is only asynchronous with respect to the host: block on it so a
+        # state_dict() / checkpoint taken right after (before any outer step) never reads a partial
+        # snapshot; device-resident snapshots stay stream-ordered
+        host = self.snapshot.device.type == "cpu"
+        self.snapshot.copy_(self.gather(), non_blocking=not host)
 
 
 class ModuleDiloco:
@@ -176,6 +180,7 @@ class ModuleDiloco:
         for g, s in zip(self.groups, d["snapshots"]):
             g.snapshot.copy_(s)
         self.outer_optimizer.load_state_dict(d["outer"])
-        self.inner_optimizer.load_state_dict(d["inner"])
+        if "inner" in d:  # optional, as in Diloco.load_state_dict (AdamW state may be kept per rank)
+            self.inner_optimizer.load_state_dict(d["inner"])
         self.scheduler.load_state_dict(d["scheduler"])
         self.local_step = int(d["local_step"])

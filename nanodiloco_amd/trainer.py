@@ -37,7 +37,7 @@ class TrainArgs:
     # ---- the 13 reference flags (REF/nanodiloco/main.py:42-56), same defaults
     seed: int = 1337
     batch_size: int = 256
-    per_device_batch_size: int = 8
+    per_device_batch_size: int = 8     # or "auto": the largest that suits the model (auto_micro_batch)
     seq_length: int = 1024
     warmup_steps: int = 100
     total_steps: int = 10_000
@@ -65,6 +65,9 @@ class TrainArgs:
     legacy_grad_sum: bool = False
     activation_checkpointing: bool = False
     fp8: bool = False              # fp8 e4m3/e5m2 decoder projections (GPU, bf16 compute)
+    fp8_wgrad: bool = False        # with fp8: the weight-gradient GEMMs in fp8 too
+    force_collectives: bool = False  # world size 1: still create a (one-rank) process group and issue
+                                     # every collective (exercises the RCCL path on one GPU)
     tuned_gemm: bool = True        # load the pre-tuned hipBLASLt algorithm table (ops/tuned_gemm.py)
     hip_graph: str = "auto"        # capture the micro-batch fwd+bwd in a HIP graph (utils/graphs.py):
                                    # on | off | auto (= on for launch-bound models: GPU, < 100M params,
@@ -96,6 +99,36 @@ def _dtype(name: str, device: torch.device) -> torch.dtype:
             "bfloat16": torch.bfloat16, "fp8": torch.bfloat16}[name]
 
 
+# activation budget of one micro-batch as a share of device memory, and the micro-batch token target
+# (64 x 1024: the best of 16/32/64/128/256 sequences for Llama-150M on MI355X, docs/DESIGN.md §6)
+_AUTO_MEM_SHARE = 0.3
+_AUTO_TOKENS = 65536
+
+
+def auto_micro_batch(cfg: LlamaConfig, seq_len: int, batch_size: int, device: torch.device) -> int:
+    """``--per-device-batch-size auto``: the largest divisor of ``batch_size`` whose micro-batch holds at
+    most ~64k tokens and whose activations (flash attention, no recompute: ~34 * d bytes per token and
+    layer in bf16, plus the chunked lm-head's 4 GiB logits budget) fit in 30 % of the device memory.
+
+    The math does not change: gradients are the mean over the micro-batches of an inner step (each
+    micro-batch a mean over its tokens), so with equal tokens per micro-batch (synthetic / packed
+    data) any micro-batch size gives the same update up to summation order.  With padded HF batches
+    the per-micro-batch token counts differ, exactly as they do for the reference's micro-batch 8.
+    On CPU the reference's default (8) is kept."""
+    if device.type != "cuda":
+        cap = 8
+    else:
+        mem = torch.cuda.get_device_properties(device).total_memory
+        per_tok = 34 * cfg.hidden_size * cfg.num_hidden_layers + 8 * cfg.hidden_size
+        budget = _AUTO_MEM_SHARE * mem - (4 << 30)
+        cap = max(1, min(_AUTO_TOKENS, int(budget // per_tok)) // max(1, seq_len))
+    mb = 1
+    for cand in range(1, batch_size + 1):
+        if batch_size % cand == 0 and cand <= cap:
+            mb = cand
+    return mb
+
+
 def _resolve_data_kind(a: TrainArgs) -> str:
     if a.data != "auto":
         return a.data
@@ -111,20 +144,23 @@ def _resolve_data_kind(a: TrainArgs) -> str:
 class Trainer:
     def __init__(self, args: TrainArgs, env: Optional[DistEnv] = None):
         self.args = a = args
-        if a.batch_size % a.per_device_batch_size:
-            raise ValueError("batch_size must be a multiple of per_device_batch_size")  # REF main.py:65
         if a.total_steps % a.inner_steps:
             raise ValueError("total_steps must be a multiple of inner_steps")  # REF main.py:69
         ops.set_backend(a.ops)
         ops.set_wgrad_overlap(a.wgrad_overlap)
         ops.set_deterministic(a.deterministic)
         self.env = env or init_distributed(a.backend, a.inner_dp, device=None if a.device == "auto" else a.device,
-                                           timeout_s=a.collective_timeout_s)
+                                           timeout_s=a.collective_timeout_s, force_pg=a.force_collectives)
         e = self.env
         if e.device.type == "cuda" and a.tuned_gemm:
             from .ops.tuned_gemm import enable_tuned_gemms
             enable_tuned_gemms(e.device)
         self.llama_config: LlamaConfig = resolve_llama_config(a.llama_config_file)
+        if str(a.per_device_batch_size).lower() == "auto":
+            a.per_device_batch_size = auto_micro_batch(self.llama_config, a.seq_length, a.batch_size, e.device)
+        a.per_device_batch_size = int(a.per_device_batch_size)
+        if a.batch_size % a.per_device_batch_size:
+            raise ValueError("batch_size must be a multiple of per_device_batch_size")  # REF main.py:65
         self.run_config = load_config_from_file(a.wandb_config_file) if a.wandb_config_file else default_run_config()
         set_seed_all(a.seed)
         self.grad_accum = a.batch_size // a.per_device_batch_size
@@ -132,7 +168,7 @@ class Trainer:
         self.compute_dtype = _dtype(a.dtype, e.device)
         self.model = LlamaForCausalLM(self.llama_config, e.device, self.compute_dtype,
                                       activation_checkpointing=a.activation_checkpointing,
-                                      fp8=a.fp8 or a.dtype == "fp8").init_weights(a.seed)
+                                      fp8=a.fp8 or a.dtype == "fp8", fp8_wgrad=a.fp8_wgrad).init_weights(a.seed)
         inner = FlatAdamW(self.model.store, lr=a.lr, weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm,
                           skip_nonfinite=a.skip_nonfinite)
         outer = FlatOuterNesterov(self.model.store, lr=a.outer_lr, momentum=a.outer_momentum)
@@ -166,8 +202,10 @@ class Trainer:
         self.graphed = None
         hg = str(a.hip_graph).lower()
         if hg == "auto":
+            # HF batches always carry an attention_mask, which the captured graph does not take:
+            # never capture (and hold the graph's memory) for a data source that produces masks
             use_graph = (e.device.type == "cuda" and e.inner_dp == 1 and self.model.fp8 is None
-                         and self.llama_config.num_params() < 100_000_000)
+                         and self.data_kind != "hf" and self.llama_config.num_params() < 100_000_000)
         else:
             use_graph = hg in ("1", "true", "on", "yes")
         if use_graph:

@@ -270,6 +270,23 @@ def test_wgrad_gemm(M, N, K, variant, monkeypatch):
     assert torch.equal(gw, gw2)  # deterministic (no atomics)
 
 
+@pytest.mark.parametrize("variant", ["", "reg", "dma0", "4w"])
+def test_wgrad_no_empty_split_with_poisoned_slabs(variant, monkeypatch):
+    """K = 41 * 64 over 16 output tiles: rounding the per-split K chunk up to whole tiles would leave the
+    last split empty; its slab plane must not be summed stale (the workspace is NaN-poisoned first)."""
+    monkeypatch.setenv("ND_WGRAD_VARIANT", variant)
+    from nanodiloco_amd.ops import gemm as G
+    M = N = 1024
+    K = 41 * 64
+    G._workspace(torch.device(DEV), 16 * M * N).fill_(float("nan"))
+    dy = torch.randn(K, M, device=DEV).bfloat16()
+    x = torch.randn(K, N, device=DEV).bfloat16()
+    gw = torch.zeros(M, N, device=DEV)
+    G.wgrad(gw, dy, x)
+    assert torch.isfinite(gw).all()
+    assert rel(gw, dy.float().t() @ x.float()) < 1e-5
+
+
 def test_wgrad_strided_views():
     """Operands that are column slices of a wider buffer (fused q|k|v grads)."""
     from nanodiloco_amd.ops.gemm import wgrad

@@ -1,0 +1,45 @@
+"""The RCCL (``nccl`` backend) path on one MI355X: tests/_rccl_check.py in its own process (a one-rank
+process group must not leak into the other tests), and bench.py under torchrun with ``--backend
+nccl`` so the headline JSON reports a live RCCL communicator and its per-phase outer-step spans."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from ._mp import free_port
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(autouse=True)
+def _gpu(hip_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def test_rccl_one_rank_collectives_diloco_and_hooks():
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "_rccl_check.py")], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "RCCL_CHECK_PASSED" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_bench_torchrun_one_rank_nccl():
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "1", "--backend", "nccl",
+           "--model", "llama_tiny.json", "--batch-size", "16", "--micro-batch", "8", "--seq-len", "256",
+           "--steps", "4", "--warmup", "1", "--inner-steps", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    j = json.loads(lines[0])
+    assert j["comm_backend"] == "nccl" and j["allreduce_calls_per_outer_step"] >= 1
+    assert j["step_driver"] == "Trainer.inner_step" and j["outer_steps_in_window"] == 2
+    ph = j["outer_phase_ms"]
+    assert ph is not None and set(ph) == {"pseudograd", "allreduce", "outer_update"}
