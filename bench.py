@@ -72,8 +72,12 @@ def parse():
                     help="attention backward: row statistics inside the dQ kernel (0: separate passes)")
     ap.add_argument("--dgrad-t", type=int, default=1, choices=[0, 1],
                     help="input-gradient GEMMs on transposed weight copies (K-contiguous NT layout)")
-    ap.add_argument("--fused-swiglu", type=int, default=0, choices=[0, 1],
-                    help="gate|up GEMM with SwiGLU in the own GEMM's epilogue (1) or hipBLASLt + swiglu kernel (0)")
+    ap.add_argument("--proj-gemm", default="pp", choices=["pp", "blas"],
+                    help="projection / lm-head GEMMs: own ping-pong MFMA kernel (pp) or hipBLASLt (blas, A/B)")
+    ap.add_argument("--fused-rope", type=int, default=1, choices=[0, 1],
+                    help="RoPE in the q|k|v GEMM epilogue (own kernel) vs a separate rotation pass")
+    ap.add_argument("--fused-mlp", type=int, default=1, choices=[0, 1],
+                    help="SwiGLU in the gate|up GEMM epilogue and its backward in the down dgrad epilogue")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
     ap.add_argument("--fp8-wgrad", action="store_true", help="with --fp8: weight-gradient GEMM in fp8 too")
     ap.add_argument("--fp8-gemm", default="hipblaslt", choices=["hip", "hipblaslt"],
@@ -87,7 +91,8 @@ def parse():
 def main():
     a = parse()
     # kernel-path switches the trainer does not own (A/B flags); set before the model is built
-    ops.set_fused_swiglu(bool(a.fused_swiglu))
+    ops.set_proj_gemm(a.proj_gemm)
+    ops.set_fused_epilogues(rope=bool(a.fused_rope), mlp=bool(a.fused_mlp))
     ops.set_dgrad_transposed(bool(a.dgrad_t))
     ops.set_attn_fused_stats(bool(a.attn_fused_stats))
     if a.fp8:
@@ -224,7 +229,8 @@ def main():
             "final_loss": round(final_loss, 4),
             "tuned_gemm": enable_tuned_gemms(env.device) if env.device.type == "cuda" and not a.no_tuned_gemm else False,
             "wgrad_overlap": ops.wgrad_overlap_enabled(),
-            "fused_swiglu_gemm": ops.fused_swiglu_enabled(),
+            "proj_gemm": ops.proj_gemm(),
+            "fused_epilogues": ops.fused_epilogues(),
             "fp8_gemm": a.fp8_gemm if a.fp8 else None,
             "dgrad_transposed": ops.dgrad_transposed_enabled(),
             "ops": ops.get_backend() if a.ops != "auto" else ("hip" if env.device.type == "cuda" else "torch"),

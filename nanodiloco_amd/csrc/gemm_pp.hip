@@ -1,0 +1,611 @@
+// Ping-pong projection GEMM for gfx950 (round 3): C[M, N] = A[M, K] . B[N, K]^T, bf16 in, fp32
+// accumulate -- the forward and input-gradient GEMMs of every Llama projection (B = W[out, in], or its
+// transposed copy W^T[in, out] for dgrad) and the lm-head logits / dgrad.
+//
+// Why a new structure (docs/DESIGN.md §3): the round-2 four-wave kernel (one MFMA wave per SIMD)
+// stalls its matrix pipe whenever its only wave waits on LDS reads, LDS-DMA issue or a barrier
+// (43 % MFMA busy vs hipBLASLt's 63 %).  Here every SIMD holds TWO waves with opposite roles:
+//
+//   * 512 threads = 8 waves = two groups of four; waves 0-3 (group 0) and 4-7 (group 1) each cover all
+//     four SIMDs once, so every SIMD pairs one wave of each group (MI355X_MICROARCH "Two waves per
+//     SIMD", item 9: split roles by wave number >= 4).
+//   * 256 x 256 output tile, BK = 64; group g owns tile rows 128 g .. 128 g + 127, wave w & 3 owns
+//     64 columns: 128 x 64 per wave = 8 x 4 v_mfma_f32_16x16x32_bf16 accumulators (128 AGPRs) plus
+//     one K-tile of fragments (8 + 4 blocks x 2 k-steps of bf16x8 = 96 VGPRs): 2 waves / SIMD.
+//   * Each K-tile is two phases per group, LOAD (all 24 ds_read_b128 fragment reads of the K-tile,
+//     this group's LDS-DMA pieces, lgkmcnt(0)) and COMPUTE (64 MFMAs from registers), and group 1 runs
+//     ONE BARRIER BEHIND group 0:
+//
+//         barrier:      ... | 2s      | 2s+1       | 2s+2       | ...
+//         group 0:          LOAD(s)   COMPUTE(s)   LOAD(s+1)
+//         group 1:          COMPUTE(s-1) LOAD(s)   COMPUTE(s)
+//
+//     so while one wave of a SIMD issues its MFMA chain (s_setprio 1) its partner issues the loads of
+//     the other half of the tile: the matrix pipe never waits for LDS, DMA issue or the barrier.
+//
+// LDS: two 64-KiB K-tile buffers of four 16-KiB half-tiles (A0 = tile rows 0-127, A1 = 128-255, B0, B1),
+// [128 rows][64 k] with the 16-B chunk index XOR-swizzled by (row >> 1) & 7 (on the DMA SOURCE
+// address -- LDS-DMA writes lane-linear -- and on the ds_read_b128 reads): every 16-lane group of a
+// fragment read hits 16 distinct bank slots.  DMA ownership (derived from the phase table above,
+// each buffer restaged only after both groups' reads of it have retired):
+//
+//   group 0, LOAD(s): B0 + B1 of K-tile s+1   (8 pieces / wave; retired by vmcnt at the end of
+//                                              its COMPUTE(s), read from LOAD(s+1) on)
+//   group 1, LOAD(s): A1 of K-tile s+1, then A0 of K-tile s+2 (4 + 4 pieces / wave; A1(s+1) retired
+//                     at the end of its COMPUTE(s), A0(s+2) at the end of its LOAD(s+1))
+//
+// The waits are counted (`s_waitcnt vmcnt(N)`, never a drain of the whole stream), and the pieces go
+// through buffer descriptors whose record count ends at the operand's last row, so the M / N tail
+// rows read as out-of-range (no clamping, tile-independent per-lane offsets).
+//
+// Persistent: one workgroup per CU walks tiles first, first + G, ... (XCD-remapped; GM m-panels per
+// group of tiles so one XCD's 32 concurrent tiles share A / B panels in its L2), and the K-tile
+// stream -- DMA, fragment reads, MFMAs -- runs across tile boundaries.  A tile's epilogue (fused
+// variants below) is issued inside the next tile's first LOAD phase, behind that phase's DMA, with
+// 16-B buffer stores the counted waits leave in flight.
+//
+// Fused epilogues (each removes a separate HBM round trip of the [M, N] output):
+//   PP_STORE    C = bf16(acc)
+//   PP_ROPE     q|k|v projection: RoPE (half-split, head_dim HD = 32 / 64) on the q and k columns of
+//               the fp32 accumulator before the one bf16 rounding; v columns stored plainly
+//   PP_SWIGLU   gate|up projection, 128 gate / up units per tile (wave column group = 32 gate rows
+//               then the 32 matching up rows of the weight): stores gu = [gate | up] AND
+//               act = silu(gate) * up
+//   PP_DSWIGLU  down-projection input gradient: acc = d(act); reads gate / up, stores d(gate | up)
+//
+// Reference role: every nn.Linear of HF LlamaForCausalLM (/root/reference/nanodiloco/main.py:97-99,
+// run at :109-111).
+#include "common.h"
+#include <cstdlib>
+#include <type_traits>
+
+using namespace nd;
+
+namespace {
+typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
+constexpr int TM = 256, TN = 256, TK = 64;
+constexpr uint32_t HALF_B = 128 * TK * 2;  // bytes of one half-tile (16 KiB)
+constexpr uint32_t BUF_B = 4 * HALF_B;     // bytes of one K-tile buffer (64 KiB)
+constexpr int LGKM0 = 0xC07F;              // s_waitcnt lgkmcnt(0), vmcnt / expcnt at their maxima
+
+enum : int { PP_STORE = 0, PP_ROPE = 1, PP_SWIGLU = 2, PP_DSWIGLU = 3 };
+
+struct PPEpi {
+  const float* cosT;  // PP_ROPE: fp32 [T, hd] tables (HF cat(freqs, freqs) layout)
+  const float* sinT;
+  int T, rope_cols;
+  bf16_t* act;        // PP_SWIGLU: act [M, F]
+  int64_t ld_act;
+  const bf16_t* gu;   // PP_DSWIGLU: gu [M, 2F]
+  int64_t ld_gu;
+};
+
+// stores per wave per tile epilogue (counted by the vmcnt waits that follow it)
+template <int EPI> struct NStores { static constexpr int v = EPI == PP_SWIGLU ? 24 : EPI == PP_DSWIGLU ? 32 : 16; };
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+// one LDS-DMA wave-instruction: 64 lanes x 16 B from descriptor r at per-lane byte offset voff to
+// LDS [lds, lds + 1 KiB); lanes past the descriptor's record count read nothing (tail rows)
+__device__ __forceinline__ void dma(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds) : "memory");
+}
+// accumulator pinned to AGPRs (tied operand): the chain on one accumulator needs no wait states;
+// compiler code reading the result waits for drain()
+#ifndef ND_PP_ASM_MFMA
+__device__ __forceinline__ void mma(const bf16x8& a, const bf16x8& b, f32x4& c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bfv8, a), __builtin_bit_cast(bfv8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ void mma0(const bf16x8& a, const bf16x8& b, f32x4& c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bfv8, a), __builtin_bit_cast(bfv8, b), f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+}
+#else
+__device__ __forceinline__ void mma(const bf16x8& a, const bf16x8& b, f32x4& c) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+// first k-step of a tile: zero accumulator input (no per-tile AGPR zeroing)
+__device__ __forceinline__ void mma0(const bf16x8& a, const bf16x8& b, f32x4& c) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+}
+#endif
+__device__ __forceinline__ void drain() { asm volatile("s_nop 15\n\ts_nop 3" ::: "memory"); }
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+template <int N> __device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+// runtime count out of a small compile-time set (wave-uniform branch)
+template <int NST> __device__ __forceinline__ void vmwait_n(int n) {
+  switch (n) {
+    case 0: vmwait<0>(); break;
+    case 4: vmwait<4>(); break;
+    case 8: vmwait<8>(); break;
+    case NST: vmwait<NST>(); break;
+    case NST + 4: vmwait<NST + 4>(); break;
+    case NST + 8: vmwait<NST + 8>(); break;
+    default: vmwait<0>(); break;
+  }
+}
+
+// bf16-pack the 4-column quads of two adjacent 16-column blocks (x = block b, y = block b + 1) and
+// v_permlane16_swap them: lane row q = lane >> 4 then holds 8 consecutive columns
+// (block b + (q & 1), columns 8 (q >> 1) .. + 7) -> one 16-B store
+__device__ __forceinline__ u32x4 pair16(const f32x4& x, const f32x4& y) {
+  const auto s0 = __builtin_amdgcn_permlane16_swap(pack2(x[0], x[1]), pack2(y[0], y[1]), false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(pack2(x[2], x[3]), pack2(y[2], y[3]), false, false);
+  u32x4 d = u32x4{s0[0], s1[0], s0[1], s1[1]};
+  asm volatile("s_nop 1" : "+v"(d));  // permlane result -> store data: two wait states
+  return d;
+}
+__device__ __forceinline__ float rbf(float x) { return lo_bf(pack2(x, 0.f)); }
+__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+
+// ABL: ablation builds for profiling only (wrong results): 1 no LDS-DMA in the loop, 2 fragments
+// read only in each tile's first K-tile, 4 no barriers in the loop, 8 no epilogue stores
+template <int EPI, int HD, int ABL = 0>
+__global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                         bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                         int64_t ldb, int64_t ldc, PPEpi ep, int GM, int stagger) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NST = NStores<EPI>::v;
+  constexpr int STP = (ABL & 32) ? 2 : 0;  // C-store cache policy (ablation 32: nt)
+  constexpr int tcols = EPI == PP_SWIGLU ? 128 : TN;  // output columns (units) per tile
+  const int tn = (N + tcols - 1) / tcols, tmn = (M + TM - 1) / TM, tiles = tmn * tn;
+  const int G = gridDim.x;  // <= tiles (host)
+  const int first = xcd_remap(blockIdx.x, G);
+  const int my_tiles = (tiles - 1 - first) / G + 1;
+  const int nk = K / TK;
+  const int total = my_tiles * nk;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = w >> 2, wn = w & 3;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+
+  // tile t -> (m0, n0): groups of GM m-panels walked n-major inside the group
+  auto coords = [&](int t, int& m0, int& n0) __attribute__((always_inline)) {
+    if (GM <= 1) {
+      m0 = (t / tn) * TM;
+      n0 = (t % tn) * tcols;
+    } else {
+      const int per = GM * tn, grp = t / per, r = t - grp * per;
+      const int gm = (tmn - grp * GM) < GM ? (tmn - grp * GM) : GM;
+      m0 = (grp * GM + r % gm) * TM;
+      n0 = (r / gm) * tcols;
+    }
+  };
+
+  // ---- per-lane DMA source offsets (bytes, relative to the half-tile's first row): piece p of this
+  // wave = half-tile rows 8 j .. 8 j + 7, j = wn + 4 p; lane -> row 8 j + lane / 8, logical chunk
+  // (lane & 7) ^ swizzle(row)
+  uint32_t voff[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int hr = 8 * (wn + 4 * p) + (lane >> 3);
+    const int lch = (lane & 7) ^ ((hr >> 1) & 7);
+    int row = hr;
+    if (g == 0 && EPI == PP_SWIGLU) row = ((hr >> 5) & 1) * N + (hr >> 6) * 32 + (hr & 31);  // gate | up rows
+    voff[p] = (uint32_t)(((int64_t)row * (g == 0 ? ldb : lda) + lch * 8) * 2);
+  }
+  // descriptor of one half-tile of K-tile kt of tile t: A half h (rows m0 + 128 h ..) or B half h
+  auto a_rsrc = [&](int m0, int kt, int h) __attribute__((always_inline)) {
+    const int64_t e0 = (int64_t)(m0 + 128 * h) * lda + (int64_t)kt * TK;
+    const int64_t lim = (int64_t)M * lda - e0;  // elements to the end of the operand's last row
+    return rsrc(A + e0, (uint32_t)(lim > 0 ? (lim < 0x3fffffff ? lim * 2 : 0x7ffffffe) : 0));
+  };
+  auto b_rsrc = [&](int n0, int kt, int h) __attribute__((always_inline)) {
+    const int64_t hrow = EPI == PP_SWIGLU ? 64 * h : 128 * h;  // SwiGLU: half 1 = wave groups 2, 3
+    const int64_t e0 = (int64_t)(n0 + hrow) * ldb + (int64_t)kt * TK;
+    const int64_t rows = EPI == PP_SWIGLU ? 2 * (int64_t)N : N;
+    const int64_t lim = rows * ldb - e0;
+    return rsrc(B + e0, (uint32_t)(lim > 0 ? (lim < 0x3fffffff ? lim * 2 : 0x7ffffffe) : 0));
+  };
+  // stream positions -> (tile, kt): incremental counters
+  struct Pos { int lt, kt, m0, n0; };
+  auto pos_init = [&](Pos& p, int s) __attribute__((always_inline)) {
+    p.lt = s / nk;
+    p.kt = s - p.lt * nk;
+    coords(first + p.lt * G, p.m0, p.n0);
+  };
+  auto pos_next = [&](Pos& p) __attribute__((always_inline)) {
+    if (++p.kt == nk) {
+      p.kt = 0;
+      ++p.lt;
+      if (p.lt < my_tiles) coords(first + p.lt * G, p.m0, p.n0);
+    }
+  };
+  // group 0: B (both halves) of stream position p -> buffer of p
+  auto stage_b = [&](const Pos& p, int s) __attribute__((always_inline)) {
+    const uint32_t dst = lds0 + (uint32_t)(s & 1) * BUF_B + 2 * HALF_B + (uint32_t)wn * 1024u;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const auto r = b_rsrc(p.n0, p.kt, h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dma(r, voff[q], dst + (uint32_t)h * HALF_B + (uint32_t)q * 4096u);
+    }
+  };
+  // group 1: A half h of stream position p
+  auto stage_a = [&](const Pos& p, int s, int h) __attribute__((always_inline)) {
+    const uint32_t dst = lds0 + (uint32_t)(s & 1) * BUF_B + (uint32_t)h * HALF_B + (uint32_t)wn * 1024u;
+    const auto r = a_rsrc(p.m0, p.kt, h);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dma(r, voff[q], dst + (uint32_t)q * 4096u);
+  };
+
+  // ---- fragment reads: A rows 16 a + (lane & 15) of half g, B rows (wn & 1) 64 + 16 b + (lane & 15) of
+  // half 2 + (wn >> 1); chunk (4 ks + lane / 16) ^ swizzle -- the same per-lane offset for A and B
+  const int r16 = lane & 15, q = lane >> 4;
+  const uint32_t foff0 = (uint32_t)(r16 * 128 + ((q ^ ((r16 >> 1) & 7)) << 4));
+  const uint32_t foff1 = (uint32_t)(r16 * 128 + (((4 + q) ^ ((r16 >> 1) & 7)) << 4));
+  bf16x8 fa[8][2], fb[4][2];
+  auto load_frags = [&](int s) __attribute__((always_inline)) {
+    const char* base = smem + (s & 1) * BUF_B;
+    const char* ab = base + g * HALF_B;
+    const char* bb = base + (2 + (wn >> 1)) * HALF_B + (wn & 1) * 64 * 128;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      fb[b][0] = *reinterpret_cast<const bf16x8*>(bb + b * 2048 + foff0);
+      fb[b][1] = *reinterpret_cast<const bf16x8*>(bb + b * 2048 + foff1);
+    }
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      fa[a][0] = *reinterpret_cast<const bf16x8*>(ab + a * 2048 + foff0);
+      fa[a][1] = *reinterpret_cast<const bf16x8*>(ab + a * 2048 + foff1);
+    }
+  };
+
+  f32x4 acc[8][4];
+
+  // ---- epilogue of tile t (stores: exactly NST 16-B buffer stores per wave; out-of-range lanes drop
+  // through the descriptor's record count or an offset sentinel)
+  auto epilogue = [&](int t) __attribute__((always_inline)) {
+    int m0, n0;
+    coords(t, m0, n0);
+    const int rows = M - m0 < TM ? M - m0 : TM;
+    if constexpr (EPI == PP_STORE || EPI == PP_ROPE) {
+      const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
+      constexpr int HALFD = HD / 2;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int mr = g * 128 + a * 16 + r16;  // row inside the tile
+        f32x4 v[4] = {acc[a][0], acc[a][1], acc[a][2], acc[a][3]};
+        if constexpr (EPI == PP_ROPE) {
+          // the wave's 64 columns are one 64-wide head (or two 32-wide ones): column block b pairs
+          // with b + HD / 32 in the same lane; v columns (>= rope_cols) pass through
+          const bool rot = n0 + wn * 64 < ep.rope_cols;
+          const int t = (m0 + mr) % ep.T;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            if (((b * 16) % HD) >= HALFD) continue;
+            const int p = b + HALFD / 16, i = (b * 16) % HD + 4 * q;
+            const float4 c = *reinterpret_cast<const float4*>(ep.cosT + (int64_t)t * HD + i);
+            const float4 s = *reinterpret_cast<const float4*>(ep.sinT + (int64_t)t * HD + i);
+            const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float c1 = rot ? cc[r] : 1.f, s1 = rot ? ss[r] : 0.f;
+              const float x1 = v[b][r], x2 = v[p][r];
+              v[b][r] = x1 * c1 - x2 * s1;
+              v[p][r] = x2 * c1 + x1 * s1;
+            }
+          }
+        }
+#pragma unroll
+        for (int bp = 0; bp < 2; ++bp) {
+          const int col = n0 + wn * 64 + (2 * bp + (q & 1)) * 16 + (q >> 1) * 8;
+          const uint32_t off = col < N ? (uint32_t)(((int64_t)mr * ldc + col) * 2) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b128(pair16(v[2 * bp], v[2 * bp + 1]), cr, off, 0, STP);
+        }
+      }
+    } else if constexpr (EPI == PP_SWIGLU) {
+      // lane's gate units f = n0 + 32 wn + 16 b + 4 q + r (b = 0, 1) pair with up = acc[a][b + 2]
+      const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
+      const auto ar = rsrc(ep.act + (int64_t)m0 * ep.ld_act, (uint32_t)((int64_t)rows * ep.ld_act * 2));
+      const int f = n0 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8;
+      const bool ok = f < N;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int mr = g * 128 + a * 16 + r16;
+        f32x4 g2[2], u2[2], y2[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            g2[j][r] = rbf(acc[a][j][r]);  // act from the rounded gate / up: what the backward reads
+            u2[j][r] = rbf(acc[a][j + 2][r]);
+            y2[j][r] = silu(g2[j][r]) * u2[j][r];
+          }
+        const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
+        const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
+        const uint32_t oy = ok ? (uint32_t)(((int64_t)mr * ep.ld_act + f) * 2) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(pair16(g2[0], g2[1]), cr, og, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(pair16(u2[0], u2[1]), cr, ou, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(pair16(y2[0], y2[1]), ar, oy, 0, 0);
+      }
+    } else {  // PP_DSWIGLU: acc = d(act)[m][f]; C = d(gate | up) [M, 2N]
+      const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
+      const auto gr = rsrc(ep.gu + (int64_t)m0 * ep.ld_gu, (uint32_t)((int64_t)rows * ep.ld_gu * 2));
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int mr = g * 128 + a * 16 + r16;
+#pragma unroll
+        for (int bp = 0; bp < 2; ++bp) {
+          // after the pair swap this lane holds d(act) of 8 consecutive units f .. f + 7
+          const int f = n0 + wn * 64 + (2 * bp + (q & 1)) * 16 + (q >> 1) * 8;
+          const bool ok = f < N;
+          const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ep.ld_gu + f) * 2) : 0x80000000u;
+          const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ep.ld_gu + N + f) * 2) : 0x80000000u;
+          const u32x4 gv = __builtin_amdgcn_raw_buffer_load_b128(gr, og, 0, 0);
+          const u32x4 uv = __builtin_amdgcn_raw_buffer_load_b128(gr, ou, 0, 0);
+          // d(act) as fp32 in the same 8-unit order: swap the fp32 quads like pair16 does
+          f32x4 d0, d1;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[a][2 * bp][r]),
+                                                              __float_as_uint(acc[a][2 * bp + 1][r]), false, false);
+            d0[r] = __uint_as_float(sw[0]);
+            d1[r] = __uint_as_float(sw[1]);
+          }
+          // lane row q even: d0 = units 0-3, d1 = units 4-7 of block 2 bp (cols 8 (q >> 1) ..);
+          // odd: d0 = block 2 bp + 1's units 0-3 ... -- the same (x, y) order pair16 packs
+          float dg[8], du[8];
+          const uint32_t gw[4] = {gv[0], gv[1], gv[2], gv[3]}, uw[4] = {uv[0], uv[1], uv[2], uv[3]};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = e < 4 ? d0[e] : d1[e - 4];
+            const float gg = (e & 1) ? hi_bf(gw[e >> 1]) : lo_bf(gw[e >> 1]);
+            const float uu = (e & 1) ? hi_bf(uw[e >> 1]) : lo_bf(uw[e >> 1]);
+            const float sg = 1.f / (1.f + __expf(-gg));
+            du[e] = d * gg * sg;
+            dg[e] = d * uu * sg * (1.f + gg * (1.f - sg));
+          }
+          const u32x4 og4 = u32x4{pack2(dg[0], dg[1]), pack2(dg[2], dg[3]), pack2(dg[4], dg[5]), pack2(dg[6], dg[7])};
+          const u32x4 ou4 = u32x4{pack2(du[0], du[1]), pack2(du[2], du[3]), pack2(du[4], du[5]), pack2(du[6], du[7])};
+          const uint32_t cg = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
+          const uint32_t cu = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b128(og4, cr, cg, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(ou4, cr, cu, 0, 0);
+        }
+      }
+    }
+  };
+
+  // ---- prologue: K-tile 0 complete plus A0 of K-tile 1, all waves drain, group 1 one barrier behind
+  Pos pb, pa1, pa0;  // group 0: B stream; group 1: A1 and A0 streams
+  if (g == 0) {
+    pos_init(pb, 0);
+    stage_b(pb, 0);
+    pos_next(pb);  // now K-tile 1
+  } else {
+    pos_init(pa1, 0);
+    stage_a(pa1, 0, 0);  // A0 of K-tile 0 too (A0 runs two K-tiles ahead from then on)
+    stage_a(pa1, 0, 1);
+    pos_next(pa1);  // K-tile 1
+    pos_init(pa0, total > 1 ? 1 : 0);
+    if (total > 1) {
+      stage_a(pa0, 1, 0);
+      pos_next(pa0);  // K-tile 2
+    }
+  }
+  // Stagger the workgroups' tile boundaries: every CU would otherwise finish its tiles in lockstep
+  // and all 256 store their 128-KiB C tiles at once (a 32-MiB write burst the store queues back up
+  // on -- measured ~20 % of the kernel with the stores ablated).  Workgroup b starts its stream
+  // (b % 8 + 8 ((b / 8) % 2)) * stagger cycles late, so the bursts of the 16 slots land in turn.
+  if (stagger > 0) {
+    const int slot = (int)(blockIdx.x % 8) + 8 * (int)((blockIdx.x / 8) % 2);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t d = (uint64_t)slot * (uint64_t)stagger;
+    while (__builtin_amdgcn_s_memtime() - t0 < d) __builtin_amdgcn_s_sleep(4);
+  }
+  vmwait<0>();
+  bar();
+  if (g == 1) bar();
+
+  // one K-tile: LOAD(s) + COMPUTE(s).  FIRST (the tile's first K-tile, a separate instantiation so
+  // no accumulator PHI merges two definitions): zero accumulator input, and for lt > 0 the previous
+  // tile's epilogue inside the LOAD phase
+  auto ktile = [&](auto FIRST, int s, int lt, int kt) __attribute__((always_inline)) {
+    constexpr bool F = decltype(FIRST)::value;
+    const bool fat = F && lt > 0;
+    // group 1, the K-tile after a fat phase: the previous tile's stores are younger than A0(s + 1),
+    // which this LOAD phase retires -- leave them in flight
+    const bool after_fat = !F && kt == 1 && lt > 0;
+    const bool more1 = s + 1 < total, more2 = s + 2 < total;
+    // ================= LOAD(s)
+    if (ABL & 1) {
+    } else if (g == 0) {
+      if (more1) {
+        stage_b(pb, s + 1);
+        pos_next(pb);
+      }
+    } else {
+      if (more1) {
+        stage_a(pa1, s + 1, 1);
+        pos_next(pa1);
+      }
+      if (more2) {
+        stage_a(pa0, s + 2, 0);
+        pos_next(pa0);
+      }
+    }
+    if (fat) {
+      drain();
+      if constexpr ((ABL & 8) != 0) {
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) asm volatile("" ::"v"(acc[a][b]));
+      } else {
+        epilogue(first + (lt - 1) * G);
+      }
+      // the accumulators are free only after the epilogue has read them: keep the fragment reads
+      // (96 VGPRs) from being hoisted into it
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (!(ABL & 2) || F) load_frags(s);
+    __builtin_amdgcn_s_waitcnt(LGKM0);
+    if (g == 1 && !(ABL & 16))
+      vmwait_n<NST>((more1 ? 4 : 0) + (more2 ? 4 : 0) + (fat || after_fat ? NST : 0));  // A0(s + 1) landed
+    if (!(ABL & 4)) bar();
+    // ================= COMPUTE(s)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if constexpr (F) mma0(fb[b][0], fa[a][0], acc[a][b]);
+        else mma(fb[b][0], fa[a][0], acc[a][b]);
+      }
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mma(fb[b][1], fa[a][1], acc[a][b]);
+    __builtin_amdgcn_s_setprio(0);
+    if (ABL & 16) {
+    } else if (g == 0) {
+      vmwait_n<NST>(fat ? NST : 0);  // B(s + 1) landed
+    } else {
+      vmwait_n<NST>((more2 ? 4 : 0) + (fat ? NST : 0));  // A1(s + 1) landed
+    }
+    if (!(ABL & 4)) bar();
+  };
+  for (int lt = 0, s = 0; lt < my_tiles; ++lt) {
+    ktile(std::true_type{}, s++, lt, 0);
+    for (int kt = 1; kt < nk; ++kt) ktile(std::false_type{}, s++, lt, kt);
+  }
+  drain();
+  if constexpr ((ABL & 8) == 0) epilogue(first + (my_tiles - 1) * G);
+  if (g == 0 && !(ABL & 4)) bar();  // group 1 ran one barrier more
+}
+
+int g_pp_group_m = [] {
+  const char* e = getenv("ND_GEMM_PP_GM");
+  return e ? atoi(e) : 4;
+}();
+
+int num_cus_pp() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) return 256;
+    return v;
+  }();
+  return n;
+}
+
+int g_pp_variant = 0;  // ablation builds (profiling only, wrong results): nd_gemm_pp_set_variant
+int g_pp_stagger = [] {  // cycles per stagger slot (see the kernel)
+  const char* e = getenv("ND_GEMM_PP_STAGGER");
+  return e ? atoi(e) : 0;
+}();
+
+template <int EPI, int HD, int ABL>
+int launch_pp_v(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
+                const PPEpi& ep, hipStream_t s) {
+  const size_t lds = 2 * (size_t)BUF_B;  // 128 KiB
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<EPI, HD, ABL>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return (int)attr;
+  const int tcols = EPI == PP_SWIGLU ? 128 : TN;
+  const int tiles = ((M + TM - 1) / TM) * ((N + tcols - 1) / tcols);
+  const int grid = tiles < num_cus_pp() ? tiles : num_cus_pp();
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, HD, ABL>), dim3(grid), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
+                     (bf16_t*)C, M, N, K, lda, ldb, ldc, ep, g_pp_group_m, g_pp_stagger);
+  ND_LAUNCH_CHECK();
+}
+
+template <int EPI, int HD = 64>
+int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
+              const PPEpi& ep, hipStream_t s) {
+  if constexpr (EPI == PP_STORE) {
+    switch (g_pp_variant) {
+      case 1: return launch_pp_v<EPI, HD, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      case 2: return launch_pp_v<EPI, HD, 2>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      case 3: return launch_pp_v<EPI, HD, 3>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      case 4: return launch_pp_v<EPI, HD, 4>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      case 8: return launch_pp_v<EPI, HD, 8>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      case 15: return launch_pp_v<EPI, HD, 15>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      case 16: return launch_pp_v<EPI, HD, 16>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      case 32: return launch_pp_v<EPI, HD, 32>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      default: break;
+    }
+  }
+  return launch_pp_v<EPI, HD, 0>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+}
+
+bool pp_shapes_ok(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
+  // 16-B pieces and stores; per-lane byte offsets inside one tile stay 32-bit
+  return M > 0 && N > 0 && K > 0 && K % TK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 &&
+         lda >= K && ldb >= K && (int64_t)TM * lda * 2 < (1ll << 31) && (int64_t)TN * ldb * 2 < (1ll << 31) &&
+         (int64_t)TM * ldc * 2 < (1ll << 31);
+}
+}  // namespace
+
+// C[M, N] = A[M, K] . B[N, K]^T (bf16, fp32 accumulate).  K % 64 == 0, N % 8 == 0, lda / ldb / ldc % 8
+// == 0, 16-B aligned base pointers.
+ND_API int nd_gemm_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                      int64_t ldc, hipStream_t s) {
+  if (!pp_shapes_ok(M, N, K, lda, ldb, ldc)) return (int)hipErrorInvalidValue;
+  PPEpi ep{};
+  return launch_pp<PP_STORE>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+}
+
+// q|k|v projection with RoPE on the first rope_cols columns (q and k heads): rows are tokens
+// (t = row % T), tables fp32 [T, hd], hd in {32, 64}, rope_cols % 64 == 0.
+ND_API int nd_gemm_pp_rope(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                           int64_t ldc, const float* cosT, const float* sinT, int T, int hd, int rope_cols,
+                           hipStream_t s) {
+  if (!pp_shapes_ok(M, N, K, lda, ldb, ldc) || (hd != 32 && hd != 64) || rope_cols % 64 || T <= 0)
+    return (int)hipErrorInvalidValue;
+  PPEpi ep{};
+  ep.cosT = cosT; ep.sinT = sinT; ep.T = T; ep.rope_cols = rope_cols;
+  return hd == 64 ? launch_pp<PP_ROPE, 64>(A, B, C, M, N, K, lda, ldb, ldc, ep, s)
+                  : launch_pp<PP_ROPE, 32>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+}
+
+// gate|up projection + SwiGLU: B = fused weight [2F, K] (gate rows then up rows), gu = C [M, 2F]
+// (ldc), act [M, F] (ld_act).  F % 8 == 0.
+ND_API int nd_gemm_pp_swiglu(const void* A, const void* B, void* gu, void* act, int M, int F, int K, int64_t lda,
+                             int64_t ldb, int64_t ldc, int64_t ld_act, hipStream_t s) {
+  if (!pp_shapes_ok(M, F, K, lda, ldb, ldc) || ldc < 2 * (int64_t)F || ld_act % 8 || ld_act < F ||
+      (int64_t)2 * F * ldb * 2 >= (1ll << 31) || (int64_t)TM * ld_act * 2 >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  PPEpi ep{};
+  ep.act = (bf16_t*)act; ep.ld_act = ld_act;
+  return launch_pp<PP_SWIGLU>(A, B, gu, M, F, K, lda, ldb, ldc, ep, s);
+}
+
+// down-projection input gradient fused with the SwiGLU backward: d(act) = A . B^T (A = dY [M, K],
+// B = W_down^T [F, K]) is never stored; reads gu [M, 2F] and writes dgu [M, 2F].
+ND_API int nd_gemm_pp_dswiglu(const void* A, const void* B, const void* gu, void* dgu, int M, int F, int K,
+                              int64_t lda, int64_t ldb, int64_t ld_gu, int64_t ld_dgu, hipStream_t s) {
+  if (!pp_shapes_ok(M, F, K, lda, ldb, ld_dgu) || ld_gu % 8 || ld_gu < 2 * (int64_t)F || ld_dgu < 2 * (int64_t)F ||
+      (int64_t)TM * ld_gu * 2 >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  PPEpi ep{};
+  ep.gu = (const bf16_t*)gu; ep.ld_gu = ld_gu;
+  return launch_pp<PP_DSWIGLU>(A, B, dgu, M, F, K, lda, ldb, ld_dgu, ep, s);
+}
+
+ND_API int nd_gemm_pp_set_variant(int v) {
+  const int old = g_pp_variant;
+  g_pp_variant = v;
+  return old;
+}
+
+ND_API int nd_gemm_pp_set_stagger(int cycles) {
+  const int old = g_pp_stagger;
+  if (cycles >= 0) g_pp_stagger = cycles;
+  return old;
+}
+
+ND_API int nd_gemm_pp_set_group_m(int gm) {
+  const int old = g_pp_group_m;
+  if (gm >= 0) g_pp_group_m = gm;
+  return old;
+}

@@ -7,11 +7,11 @@ weights load here.  The compute graph is our own:
   h0  = embed(ids)                          fp32 residual stream, gathered from the fp32 master
   y   = rmsnorm(h0) * w_in[0]               compute dtype (bf16)
   per layer:
-    qkv = y @ [Wq|Wk|Wv]^T                  ONE GEMM (fused view of the flat buffer)
-    o   = flash_attn(rope(qkv))             HIP kernel, reads packed qkv, writes [N, nh*hd]
+    qkv = rope(y @ [Wq|Wk|Wv]^T)            ONE GEMM (fused view of the flat buffer), RoPE in its epilogue
+    o   = flash_attn(qkv)                   HIP kernel, reads packed qkv, writes [N, nh*hd]
     y,h = add_rmsnorm(h, o @ Wo^T, w_post)  residual add fused into the norm
-    gu  = y @ [Wgate|Wup]^T                 ONE GEMM
-    y,h = add_rmsnorm(h, swiglu(gu) @ Wdown^T, w_in[i+1] or w_final)
+    act = swiglu(y @ [Wgate|Wup]^T)         ONE GEMM, SwiGLU in its epilogue (SwiGLU backward in the
+    y,h = add_rmsnorm(h, act @ Wdown^T, ..) down projection's dgrad epilogue)
   loss = lm_head_ce(y, W_lm, targets)       fused chunked GEMM + CE (+ its backward)
 
 Weight gradients are written straight into ``store.grad`` by the ops' backward (and, for the
@@ -186,9 +186,18 @@ class LlamaForCausalLM:
         cdt = self.compute_dtype
         eps = c.rms_norm_eps
         qn = self._qkv_names[i]
-        qkv = self._linear(f"{i}.qkv", y, self._fused(qn, "shadow"), self._fused(qn, "grad"), y8)
+        w_qkv = self._fused(qn, "shadow")
+        rope_cols = (c.num_attention_heads + c.num_key_value_heads) * c.head_dim
+        wt_qkv = self._wt(f"{i}.qkv", w_qkv) if self.fp8 is None else None
+        if self.fp8 is None and ops.linear_rope_supported(y, w_qkv, wt_qkv, c.head_dim, rope_cols):
+            # own GEMM with RoPE on q|k in its epilogue: the attention skips its rotation pass
+            qkv = ops.linear_rope(y, w_qkv, self._fused(qn, "grad"), wt_qkv, cos, sin, T, c.head_dim, rope_cols)
+            rotated = True
+        else:
+            qkv = self._linear(f"{i}.qkv", y, w_qkv, self._fused(qn, "grad"), y8)
+            rotated = False
         o = ops.attention(qkv, cos, sin, B, T, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
-                          inplace=True, kstart=kstart)
+                          inplace=True, kstart=kstart, rotated=rotated)
         a = self._linear(f"{i}.o", o, self._w(p + "self_attn.o_proj.weight"), self._g(p + "self_attn.o_proj.weight"))
         q_gu = self._q8(f"{i}.gu")
         y, h = ops.add_rmsnorm(h, a, self._m(p + "post_attention_layernorm.weight"),
@@ -196,15 +205,19 @@ class LlamaForCausalLM:
                                q8=q_gu, q8_bwd=self._q8(f"{i}.o", grad=True))
         gn = self._gu_names[i]
         w_gu = self._fused(gn, "shadow")
+        w_dn = self._w(p + "mlp.down_proj.weight")
+        if self.fp8 is None:
+            wt_gu, wt_dn = self._wt(f"{i}.gu", w_gu), self._wt(f"{i}.down", w_dn)
+            if ops.mlp_fused_supported(y, w_gu, wt_gu, w_dn, wt_dn):
+                # own GEMMs with SwiGLU in the gate|up epilogue and its backward in the down dgrad's
+                m = ops.mlp_fused(y, w_gu, self._fused(gn, "grad"), wt_gu, w_dn,
+                                  self._g(p + "mlp.down_proj.weight"), wt_dn)
+                return m, h
         q_down = self._q8(f"{i}.down")
-        if self.fp8 is None and ops.linear_swiglu_supported(y, w_gu):
-            # own GEMM with SwiGLU in its epilogue (ops/linear.py LinearSwiGLUFn)
-            act = ops.linear_swiglu(y, w_gu, self._fused(gn, "grad"), self._wt(f"{i}.gu", w_gu))
-        else:
-            gu = self._linear(f"{i}.gu", y, w_gu, self._fused(gn, "grad"), q_gu.out if q_gu is not None else None)
-            act = ops.swiglu(gu, q8=q_down, q8_bwd=self._q8(f"{i}.gu", grad=True))
-        m = self._linear(f"{i}.down", act, self._w(p + "mlp.down_proj.weight"),
-                         self._g(p + "mlp.down_proj.weight"), q_down.out if q_down is not None else None)
+        gu = self._linear(f"{i}.gu", y, w_gu, self._fused(gn, "grad"), q_gu.out if q_gu is not None else None)
+        act = ops.swiglu(gu, q8=q_down, q8_bwd=self._q8(f"{i}.gu", grad=True))
+        m = self._linear(f"{i}.down", act, w_dn, self._g(p + "mlp.down_proj.weight"),
+                         q_down.out if q_down is not None else None)
         return m, h
 
     def hidden_states(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -264,5 +277,5 @@ class LlamaForCausalLM:
         if return_logits or (labels is None and targets is None):
             with torch.no_grad():
                 B, T = input_ids.shape
-                out.logits = torch.mm(y.detach(), self._w(lm).t()).float().view(B, T, -1)
+                out.logits = ops.mm_nt(y.detach(), self._w(lm)).float().view(B, T, -1)
         return out

@@ -2,8 +2,8 @@
 PyTorch reference (``ops.reference``) for CPU tensors; see ``ops/_ext.py`` for the policy."""
 from ._ext import available as hip_available, set_backend, get_backend, ExtensionMissing
 from .linear import linear, wgrad_accumulate, set_wgrad_overlap, wgrad_overlap_enabled, join_wgrad, \
-    set_dgrad_transposed, dgrad_transposed_enabled, transpose_into, linear_swiglu, linear_swiglu_supported, \
-    set_fused_swiglu, fused_swiglu_enabled
+    set_dgrad_transposed, dgrad_transposed_enabled, transpose_into, mm_nt, set_proj_gemm, proj_gemm, \
+    set_fused_epilogues, fused_epilogues, linear_rope, linear_rope_supported, mlp_fused, mlp_fused_supported
 from .norm import rmsnorm, rmsnorm_res, add_rmsnorm
 from .embedding import embedding
 from .swiglu import swiglu

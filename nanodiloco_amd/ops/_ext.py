@@ -172,6 +172,14 @@ def _declare(L: ctypes.CDLL):
         "nd_gemm_nt_rope": [P, P, P, I, I, I, L64, L64, L64, P, P, I, I, I, P],
         "nd_gemm_nt_swiglu": [P, P, P, P, I, I, I, L64, L64, L64, L64, P],
         "nd_gemm_nt_dswiglu": [P, P, P, P, I, I, I, L64, L64, L64, L64, P],
+        # ping-pong projection GEMMs (csrc/gemm_pp.hip)
+        "nd_gemm_pp": [P, P, P, I, I, I, L64, L64, L64, P],
+        "nd_gemm_pp_rope": [P, P, P, I, I, I, L64, L64, L64, P, P, I, I, I, P],
+        "nd_gemm_pp_swiglu": [P, P, P, P, I, I, I, L64, L64, L64, L64, P],
+        "nd_gemm_pp_dswiglu": [P, P, P, P, I, I, I, L64, L64, L64, L64, P],
+        "nd_gemm_pp_set_group_m": [I],
+        "nd_gemm_pp_set_variant": [I],
+        "nd_gemm_pp_set_stagger": [I],
         # weight-gradient GEMM
         "nd_wgrad_splits": [I, I, I],
         "nd_wgrad": [P, P, P, P, I, I, I, L64, L64, L64, P],

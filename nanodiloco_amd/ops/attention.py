@@ -59,9 +59,10 @@ class FlashAttnFn(torch.autograd.Function):
     their store epilogues (rope_mode 2), so the gradient returned is w.r.t. the raw projection."""
 
     @staticmethod
-    def forward(ctx, qkv, cos, sin, B, T, nh, nkv, hd, kstart=None):
+    def forward(ctx, qkv, cos, sin, B, T, nh, nkv, hd, kstart=None, rotated=False):
         ld = qkv.shape[1]
-        _rope(qkv, cos, sin, B, T, nh, nkv, hd, inverse=False)
+        if not rotated:  # else the projection GEMM's epilogue already rotated q|k
+            _rope(qkv, cos, sin, B, T, nh, nkv, hd, inverse=False)
         k = qkv[:, nh * hd:]
         v = qkv[:, (nh + nkv) * hd:]
         o = torch.empty(B * T, nh * hd, dtype=qkv.dtype, device=qkv.device)
@@ -95,7 +96,7 @@ class FlashAttnFn(torch.autograd.Function):
                                               _ext.ptr(lse), _ext.ptr(dqkv), _ext.ptr(dk), _ext.ptr(dv), _ext.ptr(ws),
                                               B, nh, nkv, T, hd, ld, nh * hd, _ext.ptr(cos), _ext.ptr(sin),
                                               float(hd ** -0.5), 2, ks, _ext.stream_ptr(dev)), "nd_attn_bwd_fused_ks")
-            return dqkv, None, None, None, None, None, None, None, None
+            return dqkv, None, None, None, None, None, None, None, None, None
         delta = torch.empty(B, nh, T, dtype=torch.float32, device=dev)
         _ext.check(L.nd_attn_bwd_pre(_ext.ptr(o), _ext.ptr(do), _ext.ptr(delta), B, nh, T, hd, nh * hd,
                                      _ext.stream_ptr(dev)), "nd_attn_bwd_pre")
@@ -107,7 +108,7 @@ class FlashAttnFn(torch.autograd.Function):
                                     _ext.ptr(delta), _ext.ptr(dqkv), _ext.ptr(dk), _ext.ptr(dv), _ext.ptr(ws),
                                     B, nh, nkv, T, hd, ld, nh * hd, _ext.ptr(cos), _ext.ptr(sin), float(hd ** -0.5), 2,
                                     ks, _ext.stream_ptr(dev)), "nd_attn_bwd_ks")
-        return dqkv, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None
 
 
 def key_start(attention_mask: torch.Tensor) -> torch.Tensor:
@@ -129,18 +130,21 @@ def check_padding(attention_mask: torch.Tensor) -> None:
 
 
 def attention(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, B: int, T: int, nh: int, nkv: int,
-              hd: int, inplace: bool = False, kstart: torch.Tensor = None) -> torch.Tensor:
+              hd: int, inplace: bool = False, kstart: torch.Tensor = None, rotated: bool = False) -> torch.Tensor:
     """Causal self-attention with RoPE; qkv [B*T, (nh+2nkv)*hd] -> [B*T, nh*hd].
 
     ``kstart`` (int32 [B], from :func:`key_start`) masks left padding: real queries (t >= kstart[b])
     never see the pad keys t' < kstart[b] -- the reference's causal + padding mask
     (REF/nanodiloco/main.py:79-88,109 -> HF SDPA).  ``inplace=True`` lets the HIP path rotate q|k
     inside ``qkv`` itself (the model passes it for the projection output it owns); otherwise a private
-    copy is rotated."""
+    copy is rotated.  ``rotated=True``: q|k already carry RoPE (the projection GEMM's epilogue,
+    ops/linear.py LinearRopeFn); the backward still returns the gradient w.r.t. the un-rotated q|k."""
+    if rotated and not qkv.is_cuda:
+        raise ValueError("rotated=True is a GPU-path contract (fused RoPE GEMM epilogue)")
     if _ext.use_hip(qkv):
         x = qkv.contiguous()
         if not inplace and x.data_ptr() == qkv.data_ptr():
             x = x.clone()  # never rotate a caller-visible tensor
         ks = kstart.to(device=qkv.device, dtype=torch.int32).contiguous() if kstart is not None else None
-        return FlashAttnFn.apply(x, cos, sin, B, T, nh, nkv, hd, ks)
+        return FlashAttnFn.apply(x, cos, sin, B, T, nh, nkv, hd, ks, bool(rotated))
     return ref.attention_block(qkv, cos, sin, B, T, nh, nkv, hd, use_sdpa=True, kstart=kstart)

@@ -139,6 +139,78 @@ def gemm_nt_dswiglu(dy, w_down_t, gu, dgu_out=None):
     return dgu
 
 
+# ---- ping-pong kernels (csrc/gemm_pp.hip): two waves per SIMD in opposite LOAD / COMPUTE phases
+
+def pp_supported(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Can ``gemm_pp(a, b)`` run: bf16 2-D, K % 64, N % 8, 16-B aligned rows."""
+    return (_GEMM["backend"] == "hip" and a.is_cuda and _ext.get_backend() != "torch"
+            and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
+            and a.shape[1] == b.shape[1] and a.shape[1] % 64 == 0 and b.shape[0] % 8 == 0
+            and _aligned(a) and _aligned(b))
+
+
+def gemm_pp(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """out[M, N] = a[M, K] . b[N, K]^T on the ping-pong kernel."""
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_pp(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0), b.stride(0),
+                                     out.stride(0), _ext.stream_ptr(a.device)), "nd_gemm_pp")
+    return out
+
+
+def gemm_pp_rope(a, b, cos, sin, T: int, hd: int, rope_cols: int, out=None) -> torch.Tensor:
+    """q|k|v projection with RoPE on the first ``rope_cols`` columns (rows are tokens, t = row % T)."""
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_pp_rope(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0), b.stride(0),
+                                          out.stride(0), _ext.ptr(cos), _ext.ptr(sin), T, hd, rope_cols,
+                                          _ext.stream_ptr(a.device)), "nd_gemm_pp_rope")
+    return out
+
+
+def gemm_pp_swiglu(a, w_gu, gu_out=None, act_out=None):
+    """(gu, act): gu = a . w_gu^T ([M, 2F]), act = silu(gu[:, :F]) * gu[:, F:] ([M, F])."""
+    M, K = a.shape
+    F = w_gu.shape[0] // 2
+    gu = gu_out if gu_out is not None else torch.empty(M, 2 * F, dtype=a.dtype, device=a.device)
+    act = act_out if act_out is not None else torch.empty(M, F, dtype=a.dtype, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_pp_swiglu(_ext.ptr(a), _ext.ptr(w_gu), _ext.ptr(gu), _ext.ptr(act), M, F, K,
+                                            a.stride(0), w_gu.stride(0), gu.stride(0), act.stride(0),
+                                            _ext.stream_ptr(a.device)), "nd_gemm_pp_swiglu")
+    return gu, act
+
+
+def gemm_pp_dswiglu(dy, w_down_t, gu, dgu_out=None):
+    """d(gate|up) [M, 2F] of act = silu(gate) * up, where d(act) = dy . w_down_t^T (never stored)."""
+    M, K = dy.shape
+    F = w_down_t.shape[0]
+    dgu = dgu_out if dgu_out is not None else torch.empty_like(gu)
+    _ext.check(_ext.lib().nd_gemm_pp_dswiglu(_ext.ptr(dy), _ext.ptr(w_down_t), _ext.ptr(gu), _ext.ptr(dgu), M, F, K,
+                                             dy.stride(0), w_down_t.stride(0), gu.stride(0), dgu.stride(0),
+                                             _ext.stream_ptr(dy.device)), "nd_gemm_pp_dswiglu")
+    return dgu
+
+
+def set_pp_variant(v: int) -> int:
+    """Ablation builds of the ping-pong kernel (profiling only -- WRONG results): 1 no LDS-DMA in the
+    loop, 2 no fragment reads, 3 both, 4 no barriers, 8 no epilogue stores, 15 all; 0 = the kernel."""
+    return int(_ext.lib().nd_gemm_pp_set_variant(int(v)))
+
+
+def set_pp_stagger(cycles: int) -> int:
+    """Cycles per start-stagger slot of the ping-pong kernel's workgroups (0 = off); returns the old."""
+    return int(_ext.lib().nd_gemm_pp_set_stagger(int(cycles)))
+
+
+def set_pp_group_m(g: int) -> int:
+    """m-panels per tile group of the ping-pong kernel (XCD L2 locality); returns the old value."""
+    return int(_ext.lib().nd_gemm_pp_set_group_m(int(g)))
+
+
 def _workspace(device, numel):
     """Split-K slab workspace, one per (device, stream): wgrads issued on the side stream
     (ops/linear.py overlap) and on the compute stream (lm head) must not share slabs."""

@@ -127,6 +127,62 @@ def wgrad_accumulate(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor):
     gw.add_(torch.mm(dy.t(), x).float())
 
 
+# ---- which GEMM runs the projections' forward / input-gradient products (and the lm head's)
+#   "pp"   own ping-pong MFMA kernel (csrc/gemm_pp.hip; ops.gemm.gemm_pp) -- the GPU default
+#   "blas" hipBLASLt through torch.mm (A/B runs; shapes the own kernel does not take always use it)
+# plus the epilogue fusions that only exist on the own kernel (RoPE into the q|k|v projection,
+# SwiGLU into the gate|up projection, the SwiGLU backward into the down projection's dgrad)
+_PROJ = {"gemm": "pp", "rope": True, "mlp": True}
+
+
+def set_proj_gemm(name: str) -> None:
+    if name not in ("pp", "blas"):
+        raise ValueError(name)
+    _PROJ["gemm"] = name
+
+
+def proj_gemm() -> str:
+    return _PROJ["gemm"]
+
+
+def set_fused_epilogues(rope: bool = None, mlp: bool = None) -> None:
+    """RoPE-in-q|k|v-GEMM and SwiGLU-in-MLP-GEMMs fusions (own kernel only)."""
+    if rope is not None:
+        _PROJ["rope"] = bool(rope)
+    if mlp is not None:
+        _PROJ["mlp"] = bool(mlp)
+
+
+def fused_epilogues() -> dict:
+    return {"rope": _PROJ["rope"], "mlp": _PROJ["mlp"]}
+
+
+def _pp_ok(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> bool:
+    if _PROJ["gemm"] != "pp" or not a.is_cuda:
+        return False
+    from .gemm import pp_supported
+    return pp_supported(a, b) and (out is None or (out.stride(-1) == 1 and out.stride(0) % 8 == 0
+                                                   and out.data_ptr() % 16 == 0))
+
+
+def mm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """a[M, K] . b[N, K]^T on the selected projection GEMM (own kernel when it takes the shape)."""
+    if _pp_ok(a, b, out):
+        from .gemm import gemm_pp
+        return gemm_pp(a, b, out)
+    library_gemm_fence(a.device if a.is_cuda else None)
+    return torch.mm(a, b.t(), out=out) if out is not None else torch.mm(a, b.t())
+
+
+def _wgrad(gw, dy, x):
+    if gw is None:
+        return
+    if _OVERLAP["enabled"] and gw.is_cuda:
+        _wgrad_on_side_stream(gw, dy, x)
+    else:
+        wgrad_accumulate(gw, dy, x)
+
+
 class LinearFn(torch.autograd.Function):
     """``wt`` (optional) is W^T stored [in, out] contiguous: the input gradient is then dY . (W^T)^T,
     the same K-contiguous "NT" operand layout as the forward GEMM, which hipBLASLt runs 14-16 %
@@ -138,23 +194,21 @@ class LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, w if wt is None else wt)
         ctx.gw = gw
         ctx.transposed = wt is not None
-        library_gemm_fence(x.device if x.is_cuda else None)
-        return torch.mm(x, w.t())
+        return mm_nt(x, w)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dy = dy.contiguous()
         if ctx.needs_input_grad[0]:
-            library_gemm_fence(dy.device if dy.is_cuda else None)
-            dx = torch.mm(dy, w.t()) if ctx.transposed else torch.mm(dy, w)
+            if ctx.transposed:
+                dx = mm_nt(dy, w)
+            else:
+                library_gemm_fence(dy.device if dy.is_cuda else None)
+                dx = torch.mm(dy, w)
         else:
             dx = None
-        if ctx.gw is not None:
-            if _OVERLAP["enabled"] and ctx.gw.is_cuda:
-                _wgrad_on_side_stream(ctx.gw, dy, x)
-            else:
-                wgrad_accumulate(ctx.gw, dy, x)
+        _wgrad(ctx.gw, dy, x)
         return dx, None, None, None
 
 
@@ -162,62 +216,79 @@ def linear(x: torch.Tensor, w: torch.Tensor, gw: torch.Tensor, wt: torch.Tensor 
     return LinearFn.apply(x, w, gw, wt)
 
 
-_FUSED_SWIGLU = {"enabled": False}
 
 
-def set_fused_swiglu(enabled: bool) -> None:
-    """gate|up projection + SwiGLU as one own-GEMM launch with the activation in its epilogue
-    (``LinearSwiGLUFn``) vs the tuned hipBLASLt GEMM + ``swiglu_fwd`` kernel (default).  Off by
-    default: 1.05-1.08x in isolation against untuned hipBLASLt, but -0.9 % end to end against the
-    pre-tuned table (bench.py --fused-swiglu 1: 731k vs 738k tok/s, 2 interleaved rounds)."""
-    _FUSED_SWIGLU["enabled"] = bool(enabled)
+# ---------------------------------------------------------------------------------------------
+# Fused epilogues on the own GEMM (csrc/gemm_pp.hip)
+
+def linear_rope_supported(x: torch.Tensor, w: torch.Tensor, wt, hd: int, rope_cols: int) -> bool:
+    return (_PROJ["rope"] and wt is not None and _pp_ok(x, w) and hd in (32, 64) and rope_cols % 64 == 0)
 
 
-def fused_swiglu_enabled() -> bool:
-    return _FUSED_SWIGLU["enabled"]
-
-
-def linear_swiglu_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
-    from .gemm import nt_supported
-    return (_FUSED_SWIGLU["enabled"] and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2
-            and nt_supported(x, w) and (w.shape[0] // 2) % 8 == 0)
-
-
-class LinearSwiGLUFn(torch.autograd.Function):
-    """act = silu(x W_g^T) * (x W_u^T) for the fused [W_gate; W_up] weight: the own projection GEMM
-    (csrc/gemm.hip, EPI_SWIGLU) writes gu = [gate | up] (the backward's input) and act from its
-    accumulators -- no separate SwiGLU pass over gu (measured 1.05-1.08x the hipBLASLt GEMM +
-    swiglu_fwd pair, profiles/r2_gemm_ab.md).  Backward: ``nd_swiglu_bwd`` -> the usual dgrad /
-    wgrad of the fused projection (ops/linear.py semantics: W^T copy, side-stream wgrad)."""
+class LinearRopeFn(torch.autograd.Function):
+    """q|k|v projection with RoPE applied to the q and k columns in the GEMM epilogue (replaces the
+    separate in-place rotation pass over the projection output).  The attention backward returns the
+    gradient w.r.t. the UN-rotated projection (its dq/dk store epilogue applies the inverse
+    rotation), so this backward is the plain projection backward."""
 
     @staticmethod
-    def forward(ctx, x, w, gw, wt=None):
-        from .gemm import gemm_nt_swiglu
-        gu, act = gemm_nt_swiglu(x, w)
-        ctx.save_for_backward(x, w if wt is None else wt, gu)
+    def forward(ctx, x, w, gw, wt, cos, sin, T, hd, rope_cols):
+        from .gemm import gemm_pp_rope
+        ctx.save_for_backward(x, wt)
         ctx.gw = gw
-        ctx.transposed = wt is not None
-        return act
+        return gemm_pp_rope(x, w, cos, sin, T, hd, rope_cols)
 
     @staticmethod
-    def backward(ctx, dact):
-        x, w, gu = ctx.saved_tensors
-        dact = dact.contiguous()
-        n, f2 = gu.shape
-        dgu = torch.empty_like(gu)
-        _ext.check(_ext.lib().nd_swiglu_bwd(_ext.ptr(dact), _ext.ptr(gu), _ext.ptr(dgu), _ext.dtcode(gu), n, f2 // 2,
-                                            _ext.stream_ptr(gu.device)), "nd_swiglu_bwd")
-        dx = None
-        if ctx.needs_input_grad[0]:
-            library_gemm_fence(dgu.device)
-            dx = torch.mm(dgu, w.t()) if ctx.transposed else torch.mm(dgu, w)
-        if ctx.gw is not None:
-            if _OVERLAP["enabled"]:
-                _wgrad_on_side_stream(ctx.gw, dgu, x)
-            else:
-                wgrad_accumulate(ctx.gw, dgu, x)
-        return dx, None, None, None
+    def backward(ctx, dy):
+        x, wt = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = mm_nt(dy, wt) if ctx.needs_input_grad[0] else None
+        _wgrad(ctx.gw, dy, x)
+        return dx, None, None, None, None, None, None, None, None
 
 
-def linear_swiglu(x: torch.Tensor, w: torch.Tensor, gw: torch.Tensor, wt: torch.Tensor = None) -> torch.Tensor:
-    return LinearSwiGLUFn.apply(x, w, gw, wt)
+def linear_rope(x, w, gw, wt, cos, sin, T: int, hd: int, rope_cols: int) -> torch.Tensor:
+    return LinearRopeFn.apply(x, w, gw, wt, cos, sin, int(T), int(hd), int(rope_cols))
+
+
+def mlp_fused_supported(y: torch.Tensor, w_gu: torch.Tensor, wt_gu, w_down: torch.Tensor, wt_down) -> bool:
+    F = w_gu.shape[0] // 2
+    return (_PROJ["mlp"] and wt_gu is not None and wt_down is not None and _pp_ok(y, w_gu) and F % 8 == 0
+            and w_down.shape[1] == F and w_down.shape[0] % 8 == 0)
+
+
+class MLPFn(torch.autograd.Function):
+    """The whole SwiGLU MLP on the own GEMM with both activation passes fused away:
+
+      forward   gu, act = [gate|up GEMM + SwiGLU epilogue](y)      (gu kept for the backward)
+                m       = act . W_down^T
+      backward  dgu     = [down dgrad GEMM + SwiGLU-backward epilogue](dm, W_down^T copy, gu)
+                          -- d(act) is never stored
+                gW_down += dm^T act,  dy = dgu . W_gu (W_gu^T copy),  gW_gu += dgu^T y
+
+    Same math as linear(swiglu(linear(y))) (tests/test_gemm_gpu.py checks it against that chain)."""
+
+    @staticmethod
+    def forward(ctx, y, w_gu, gw_gu, wt_gu, w_down, gw_down, wt_down):
+        from .gemm import gemm_pp_swiglu
+        gu, act = gemm_pp_swiglu(y, w_gu)
+        m = mm_nt(act, w_down)
+        ctx.save_for_backward(y, gu, act, wt_gu, wt_down)
+        ctx.gw = (gw_gu, gw_down)
+        return m
+
+    @staticmethod
+    def backward(ctx, dm):
+        from .gemm import gemm_pp_dswiglu
+        y, gu, act, wt_gu, wt_down = ctx.saved_tensors
+        gw_gu, gw_down = ctx.gw
+        dm = dm.contiguous()
+        dgu = gemm_pp_dswiglu(dm, wt_down, gu)
+        _wgrad(gw_down, dm, act)
+        dy = mm_nt(dgu, wt_gu) if ctx.needs_input_grad[0] else None
+        _wgrad(gw_gu, dgu, y)
+        return dy, None, None, None, None, None, None
+
+
+def mlp_fused(y, w_gu, gw_gu, wt_gu, w_down, gw_down, wt_down) -> torch.Tensor:
+    return MLPFn.apply(y, w_gu, gw_gu, wt_gu, w_down, gw_down, wt_down)

@@ -19,6 +19,7 @@ ap.add_argument("--n", type=int, default=3072)
 ap.add_argument("--k", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--variants", default="")
+ap.add_argument("--pp", action="store_true", help="the ping-pong kernel (csrc/gemm_pp.hip) instead of gemm_nt")
 a = ap.parse_args()
 ops.set_backend("hip")
 x = (torch.rand(a.m, a.k, device="cuda") * 2 - 1).bfloat16()
@@ -27,7 +28,10 @@ out = torch.empty(a.m, a.n, device="cuda", dtype=torch.bfloat16)
 vs = [int(v) for v in a.variants.split(",")] if a.variants else [None]
 for _ in range(a.iters):
     for v in vs:
-        G.gemm_nt(x, w, out, variant=v) if v is not None else G.gemm_nt(x, w, out)
+        if a.pp:
+            G.gemm_pp(x, w, out)
+        else:
+            G.gemm_nt(x, w, out, variant=v) if v is not None else G.gemm_nt(x, w, out)
     torch.mm(x, w.t(), out=out)
 torch.cuda.synchronize()
 print("done")
