@@ -146,15 +146,171 @@ __device__ __forceinline__ u32x4 pair16(const f32x4& x, const f32x4& y) {
 __device__ __forceinline__ float rbf(float x) { return lo_bf(pack2(x, 0.f)); }
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
-// ABL: ablation builds for profiling only (wrong results): 1 no LDS-DMA in the loop, 2 fragments
-// read only in each tile's first K-tile, 4 no barriers in the loop, 8 no epilogue stores
+// ---- epilogue of one tile: the wave's 128 x 64 accumulator block (rows 128 g + .., columns 64 wn + ..)
+// of the tile at (m0, n0) -> the fused output(s).  Exactly NStores<EPI> 16-B buffer stores per wave
+// (the callers' counted waits rely on it); out-of-range lanes drop through the descriptor's record
+// count or an offset sentinel.  `smem` + 2 BUF_B + 4 KiB w: the wave's private C staging region.
+template <int EPI, int HD, int ABL>
+__device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __restrict__ C, int M, int N,
+                                            int64_t ldc, const PPEpi& ep, int m0, int n0, int g, int wn, int w,
+                                            int lane, char* smem) {
+  constexpr int STP = (ABL & 32) ? 0 : 2;
+
+    // per-lane row offsets derive from an opaque zero: otherwise LICM hoists every row's store
+    // offset out of the tile loop and keeps ~16 VGPRs live through the whole K-loop (spills)
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    const int r16 = (lane & 15) + z, q = (lane >> 4) + z;
+    if constexpr ((ABL & 128) != 0) m0 = n0 = 0;  // ablation: every tile stores over tile 0 (L2-resident)
+    const int rows = M - m0 < TM ? M - m0 : TM;
+    if constexpr (EPI == PP_STORE || EPI == PP_ROPE) {
+      const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
+      constexpr int HALFD = HD / 2;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int mr = g * 128 + a * 16 + r16;  // row inside the tile
+        f32x4 v[4] = {acc[a][0], acc[a][1], acc[a][2], acc[a][3]};
+        if constexpr (EPI == PP_ROPE) {
+          // the wave's 64 columns are one 64-wide head (or two 32-wide ones): column block b pairs
+          // with b + HD / 32 in the same lane; v columns (>= rope_cols) pass through
+          const bool rot = n0 + wn * 64 < ep.rope_cols;
+          const int t = (m0 + mr) % ep.T;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            if (((b * 16) % HD) >= HALFD) continue;
+            const int p = b + HALFD / 16, i = (b * 16) % HD + 4 * q;
+            const float4 c = *reinterpret_cast<const float4*>(ep.cosT + (int64_t)t * HD + i);
+            const float4 s = *reinterpret_cast<const float4*>(ep.sinT + (int64_t)t * HD + i);
+            const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float c1 = rot ? cc[r] : 1.f, s1 = rot ? ss[r] : 0.f;
+              const float x1 = v[b][r], x2 = v[p][r];
+              v[b][r] = x1 * c1 - x2 * s1;
+              v[p][r] = x2 * c1 + x1 * s1;
+            }
+          }
+        }
+        if constexpr ((ABL & 256) == 0) {
+          // full-line stores: two row blocks (32 rows x 128 B) through the wave's private 4-KiB LDS
+          // staging region (behind the K-tile buffers; 16-B chunk index ^ (row & 7)), read back
+          // as whole rows -- each buffer_store then writes 8 full 128-B lines instead of 16 halves
+          char* st = smem + 2 * BUF_B + w * 4096;
+          const int row = (a & 1) * 16 + r16;
+#pragma unroll
+          for (int bp = 0; bp < 2; ++bp) {
+            const int ch = (2 * bp + (q & 1)) * 2 + (q >> 1);
+            *reinterpret_cast<u32x4*>(st + row * 128 + ((ch ^ (row & 7)) << 4)) = pair16(v[2 * bp], v[2 * bp + 1]);
+          }
+          if (a & 1) {
+            asm volatile("" ::: "memory");
+            const int lc = (lane + z) & 7;
+            const int col = n0 + wn * 64 + lc * 8;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int rr = i * 8 + ((lane + z) >> 3);
+              const u32x4 d = *reinterpret_cast<const u32x4*>(st + rr * 128 + ((lc ^ (rr & 7)) << 4));
+              const int gr = g * 128 + (a - 1) * 16 + rr;
+              const uint32_t off = col < N ? (uint32_t)(((int64_t)gr * ldc + col) * 2) : 0x80000000u;
+              __builtin_amdgcn_raw_buffer_store_b128(d, cr, off, 0, STP);
+            }
+            asm volatile("" ::: "memory");
+          }
+        } else {
+#pragma unroll
+          for (int bp = 0; bp < 2; ++bp) {
+            const int col = n0 + wn * 64 + (2 * bp + (q & 1)) * 16 + (q >> 1) * 8;
+            const uint32_t off = col < N ? (uint32_t)(((int64_t)mr * ldc + col) * 2) : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b128(pair16(v[2 * bp], v[2 * bp + 1]), cr, off, 0, STP);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one row block at a time: bounded epilogue registers
+      }
+    } else if constexpr (EPI == PP_SWIGLU) {
+      // lane's gate units f = n0 + 32 wn + 16 b + 4 q + r (b = 0, 1) pair with up = acc[a][b + 2]
+      const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
+      const auto ar = rsrc(ep.act + (int64_t)m0 * ep.ld_act, (uint32_t)((int64_t)rows * ep.ld_act * 2));
+      const int f = n0 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8;
+      const bool ok = f < N;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int mr = g * 128 + a * 16 + r16;
+        f32x4 g2[2], u2[2], y2[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            g2[j][r] = rbf(acc[a][j][r]);  // act from the rounded gate / up: what the backward reads
+            u2[j][r] = rbf(acc[a][j + 2][r]);
+            y2[j][r] = silu(g2[j][r]) * u2[j][r];
+          }
+        const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
+        const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
+        const uint32_t oy = ok ? (uint32_t)(((int64_t)mr * ep.ld_act + f) * 2) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(pair16(g2[0], g2[1]), cr, og, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(pair16(u2[0], u2[1]), cr, ou, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(pair16(y2[0], y2[1]), ar, oy, 0, 0);
+      }
+    } else {  // PP_DSWIGLU: acc = d(act)[m][f]; C = d(gate | up) [M, 2N]
+      const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
+      const auto gr = rsrc(ep.gu + (int64_t)m0 * ep.ld_gu, (uint32_t)((int64_t)rows * ep.ld_gu * 2));
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int mr = g * 128 + a * 16 + r16;
+#pragma unroll
+        for (int bp = 0; bp < 2; ++bp) {
+          // after the pair swap this lane holds d(act) of 8 consecutive units f .. f + 7
+          const int f = n0 + wn * 64 + (2 * bp + (q & 1)) * 16 + (q >> 1) * 8;
+          const bool ok = f < N;
+          const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ep.ld_gu + f) * 2) : 0x80000000u;
+          const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ep.ld_gu + N + f) * 2) : 0x80000000u;
+          const u32x4 gv = __builtin_amdgcn_raw_buffer_load_b128(gr, og, 0, 0);
+          const u32x4 uv = __builtin_amdgcn_raw_buffer_load_b128(gr, ou, 0, 0);
+          // d(act) as fp32 in the same 8-unit order: swap the fp32 quads like pair16 does
+          f32x4 d0, d1;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[a][2 * bp][r]),
+                                                              __float_as_uint(acc[a][2 * bp + 1][r]), false, false);
+            d0[r] = __uint_as_float(sw[0]);
+            d1[r] = __uint_as_float(sw[1]);
+          }
+          // lane row q even: d0 = units 0-3, d1 = units 4-7 of block 2 bp (cols 8 (q >> 1) ..);
+          // odd: d0 = block 2 bp + 1's units 0-3 ... -- the same (x, y) order pair16 packs
+          float dg[8], du[8];
+          const uint32_t gw[4] = {gv[0], gv[1], gv[2], gv[3]}, uw[4] = {uv[0], uv[1], uv[2], uv[3]};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = e < 4 ? d0[e] : d1[e - 4];
+            const float gg = (e & 1) ? hi_bf(gw[e >> 1]) : lo_bf(gw[e >> 1]);
+            const float uu = (e & 1) ? hi_bf(uw[e >> 1]) : lo_bf(uw[e >> 1]);
+            const float sg = 1.f / (1.f + __expf(-gg));
+            du[e] = d * gg * sg;
+            dg[e] = d * uu * sg * (1.f + gg * (1.f - sg));
+          }
+          const u32x4 og4 = u32x4{pack2(dg[0], dg[1]), pack2(dg[2], dg[3]), pack2(dg[4], dg[5]), pack2(dg[6], dg[7])};
+          const u32x4 ou4 = u32x4{pack2(du[0], du[1]), pack2(du[2], du[3]), pack2(du[4], du[5]), pack2(du[6], du[7])};
+          const uint32_t cg = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
+          const uint32_t cu = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b128(og4, cr, cg, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(ou4, cr, cu, 0, 0);
+        }
+      }
+    }
+  }
+
+// ABL: ablation / A-B builds for profiling only (1-8, 16, 64, 128: wrong results): 1 no LDS-DMA in the
+// loop, 2 fragments read only in each tile's first K-tile, 4 no barriers in the loop, 8 no epilogue stores
 template <int EPI, int HD, int ABL = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                          bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                         int64_t ldb, int64_t ldc, PPEpi ep, int GM, int stagger) {
+                                                         int64_t ldb, int64_t ldc, PPEpi ep, int GM) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NST = NStores<EPI>::v;
-  constexpr int STP = (ABL & 32) ? 2 : 0;  // C-store cache policy (ablation 32: nt)
+  // C stores: non-temporal (aux 2) and, for the plain / RoPE epilogues, full 128-B lines staged
+  // through LDS (measured -6 % kernel time together, profiles/r3_gemm_pp.md); ABL 32 / 256 turn
+  // them off for A/B
+  constexpr int STP = (ABL & 32) ? 0 : 2;
   constexpr int tcols = EPI == PP_SWIGLU ? 128 : TN;  // output columns (units) per tile
   const int tn = (N + tcols - 1) / tcols, tmn = (M + TM - 1) / TM, tiles = tmn * tn;
   const int G = gridDim.x;  // <= tiles (host)
@@ -261,120 +417,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
 
   f32x4 acc[8][4];
 
-  // ---- epilogue of tile t (stores: exactly NST 16-B buffer stores per wave; out-of-range lanes drop
-  // through the descriptor's record count or an offset sentinel)
-  auto epilogue = [&](int t) __attribute__((always_inline)) {
-    int m0, n0;
-    coords(t, m0, n0);
-    const int rows = M - m0 < TM ? M - m0 : TM;
-    if constexpr (EPI == PP_STORE || EPI == PP_ROPE) {
-      const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
-      constexpr int HALFD = HD / 2;
-#pragma unroll
-      for (int a = 0; a < 8; ++a) {
-        const int mr = g * 128 + a * 16 + r16;  // row inside the tile
-        f32x4 v[4] = {acc[a][0], acc[a][1], acc[a][2], acc[a][3]};
-        if constexpr (EPI == PP_ROPE) {
-          // the wave's 64 columns are one 64-wide head (or two 32-wide ones): column block b pairs
-          // with b + HD / 32 in the same lane; v columns (>= rope_cols) pass through
-          const bool rot = n0 + wn * 64 < ep.rope_cols;
-          const int t = (m0 + mr) % ep.T;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            if (((b * 16) % HD) >= HALFD) continue;
-            const int p = b + HALFD / 16, i = (b * 16) % HD + 4 * q;
-            const float4 c = *reinterpret_cast<const float4*>(ep.cosT + (int64_t)t * HD + i);
-            const float4 s = *reinterpret_cast<const float4*>(ep.sinT + (int64_t)t * HD + i);
-            const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float c1 = rot ? cc[r] : 1.f, s1 = rot ? ss[r] : 0.f;
-              const float x1 = v[b][r], x2 = v[p][r];
-              v[b][r] = x1 * c1 - x2 * s1;
-              v[p][r] = x2 * c1 + x1 * s1;
-            }
-          }
-        }
-#pragma unroll
-        for (int bp = 0; bp < 2; ++bp) {
-          const int col = n0 + wn * 64 + (2 * bp + (q & 1)) * 16 + (q >> 1) * 8;
-          const uint32_t off = col < N ? (uint32_t)(((int64_t)mr * ldc + col) * 2) : 0x80000000u;
-          __builtin_amdgcn_raw_buffer_store_b128(pair16(v[2 * bp], v[2 * bp + 1]), cr, off, 0, STP);
-        }
-      }
-    } else if constexpr (EPI == PP_SWIGLU) {
-      // lane's gate units f = n0 + 32 wn + 16 b + 4 q + r (b = 0, 1) pair with up = acc[a][b + 2]
-      const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
-      const auto ar = rsrc(ep.act + (int64_t)m0 * ep.ld_act, (uint32_t)((int64_t)rows * ep.ld_act * 2));
-      const int f = n0 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8;
-      const bool ok = f < N;
-#pragma unroll
-      for (int a = 0; a < 8; ++a) {
-        const int mr = g * 128 + a * 16 + r16;
-        f32x4 g2[2], u2[2], y2[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            g2[j][r] = rbf(acc[a][j][r]);  // act from the rounded gate / up: what the backward reads
-            u2[j][r] = rbf(acc[a][j + 2][r]);
-            y2[j][r] = silu(g2[j][r]) * u2[j][r];
-          }
-        const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
-        const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
-        const uint32_t oy = ok ? (uint32_t)(((int64_t)mr * ep.ld_act + f) * 2) : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b128(pair16(g2[0], g2[1]), cr, og, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(pair16(u2[0], u2[1]), cr, ou, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(pair16(y2[0], y2[1]), ar, oy, 0, 0);
-      }
-    } else {  // PP_DSWIGLU: acc = d(act)[m][f]; C = d(gate | up) [M, 2N]
-      const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
-      const auto gr = rsrc(ep.gu + (int64_t)m0 * ep.ld_gu, (uint32_t)((int64_t)rows * ep.ld_gu * 2));
-#pragma unroll
-      for (int a = 0; a < 8; ++a) {
-        const int mr = g * 128 + a * 16 + r16;
-#pragma unroll
-        for (int bp = 0; bp < 2; ++bp) {
-          // after the pair swap this lane holds d(act) of 8 consecutive units f .. f + 7
-          const int f = n0 + wn * 64 + (2 * bp + (q & 1)) * 16 + (q >> 1) * 8;
-          const bool ok = f < N;
-          const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ep.ld_gu + f) * 2) : 0x80000000u;
-          const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ep.ld_gu + N + f) * 2) : 0x80000000u;
-          const u32x4 gv = __builtin_amdgcn_raw_buffer_load_b128(gr, og, 0, 0);
-          const u32x4 uv = __builtin_amdgcn_raw_buffer_load_b128(gr, ou, 0, 0);
-          // d(act) as fp32 in the same 8-unit order: swap the fp32 quads like pair16 does
-          f32x4 d0, d1;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[a][2 * bp][r]),
-                                                              __float_as_uint(acc[a][2 * bp + 1][r]), false, false);
-            d0[r] = __uint_as_float(sw[0]);
-            d1[r] = __uint_as_float(sw[1]);
-          }
-          // lane row q even: d0 = units 0-3, d1 = units 4-7 of block 2 bp (cols 8 (q >> 1) ..);
-          // odd: d0 = block 2 bp + 1's units 0-3 ... -- the same (x, y) order pair16 packs
-          float dg[8], du[8];
-          const uint32_t gw[4] = {gv[0], gv[1], gv[2], gv[3]}, uw[4] = {uv[0], uv[1], uv[2], uv[3]};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float d = e < 4 ? d0[e] : d1[e - 4];
-            const float gg = (e & 1) ? hi_bf(gw[e >> 1]) : lo_bf(gw[e >> 1]);
-            const float uu = (e & 1) ? hi_bf(uw[e >> 1]) : lo_bf(uw[e >> 1]);
-            const float sg = 1.f / (1.f + __expf(-gg));
-            du[e] = d * gg * sg;
-            dg[e] = d * uu * sg * (1.f + gg * (1.f - sg));
-          }
-          const u32x4 og4 = u32x4{pack2(dg[0], dg[1]), pack2(dg[2], dg[3]), pack2(dg[4], dg[5]), pack2(dg[6], dg[7])};
-          const u32x4 ou4 = u32x4{pack2(du[0], du[1]), pack2(du[2], du[3]), pack2(du[4], du[5]), pack2(du[6], du[7])};
-          const uint32_t cg = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
-          const uint32_t cu = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
-          __builtin_amdgcn_raw_buffer_store_b128(og4, cr, cg, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(ou4, cr, cu, 0, 0);
-        }
-      }
-    }
-  };
-
   // ---- prologue: K-tile 0 complete plus A0 of K-tile 1, all waves drain, group 1 one barrier behind
   Pos pb, pa1, pa0;  // group 0: B stream; group 1: A1 and A0 streams
   if (g == 0) {
@@ -392,16 +434,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
       pos_next(pa0);  // K-tile 2
     }
   }
-  // Stagger the workgroups' tile boundaries: every CU would otherwise finish its tiles in lockstep
-  // and all 256 store their 128-KiB C tiles at once (a 32-MiB write burst the store queues back up
-  // on -- measured ~20 % of the kernel with the stores ablated).  Workgroup b starts its stream
-  // (b % 8 + 8 ((b / 8) % 2)) * stagger cycles late, so the bursts of the 16 slots land in turn.
-  if (stagger > 0) {
-    const int slot = (int)(blockIdx.x % 8) + 8 * (int)((blockIdx.x / 8) % 2);
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    const uint64_t d = (uint64_t)slot * (uint64_t)stagger;
-    while (__builtin_amdgcn_s_memtime() - t0 < d) __builtin_amdgcn_s_sleep(4);
-  }
   vmwait<0>();
   bar();
   if (g == 1) bar();
@@ -417,22 +449,36 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
     const bool after_fat = !F && kt == 1 && lt > 0;
     const bool more1 = s + 1 < total, more2 = s + 2 < total;
     // ================= LOAD(s)
-    if (ABL & 1) {
-    } else if (g == 0) {
-      if (more1) {
-        stage_b(pb, s + 1);
-        pos_next(pb);
+    auto issue_dma = [&]() __attribute__((always_inline)) {
+      if (ABL & 1) {
+      } else if (g == 0) {
+        if (more1) {
+          stage_b(pb, s + 1);
+          pos_next(pb);
+        }
+      } else {
+        if (more1) {
+          stage_a(pa1, s + 1, 1);
+          pos_next(pa1);
+        }
+        if (more2) {
+          stage_a(pa0, s + 2, 0);
+          pos_next(pa0);
+        }
       }
-    } else {
-      if (more1) {
-        stage_a(pa1, s + 1, 1);
-        pos_next(pa1);
-      }
-      if (more2) {
-        stage_a(pa0, s + 2, 0);
-        pos_next(pa0);
+    };
+    // ABL 64: fragment reads ahead of the DMA issue in the plain phases (their latency then runs
+    // under the DMA issue); a fat phase keeps DMA -> stores -> reads (the stores must be the youngest)
+    bool reads_first = false;
+    if constexpr ((ABL & 64) != 0) {
+      reads_first = !fat;
+      if (reads_first) {
+        load_frags(s);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
+    issue_dma();
     if (fat) {
       drain();
       if constexpr ((ABL & 8) != 0) {
@@ -441,14 +487,16 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
 #pragma unroll
           for (int b = 0; b < 4; ++b) asm volatile("" ::"v"(acc[a][b]));
       } else {
-        epilogue(first + (lt - 1) * G);
+        int m0, n0;
+        coords(first + (lt - 1) * G, m0, n0);
+        pp_epilogue<EPI, HD, ABL>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem);
       }
       // the accumulators are free only after the epilogue has read them: keep the fragment reads
       // (96 VGPRs) from being hoisted into it
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (!(ABL & 2) || F) load_frags(s);
+    if (!reads_first && (!(ABL & 2) || F)) load_frags(s);
     __builtin_amdgcn_s_waitcnt(LGKM0);
     if (g == 1 && !(ABL & 16))
       vmwait_n<NST>((more1 ? 4 : 0) + (more2 ? 4 : 0) + (fat || after_fat ? NST : 0));  // A0(s + 1) landed
@@ -480,9 +528,14 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
     for (int kt = 1; kt < nk; ++kt) ktile(std::false_type{}, s++, lt, kt);
   }
   drain();
-  if constexpr ((ABL & 8) == 0) epilogue(first + (my_tiles - 1) * G);
+  if constexpr ((ABL & 8) == 0) {
+    int m0, n0;
+    coords(first + (my_tiles - 1) * G, m0, n0);
+    pp_epilogue<EPI, HD, ABL>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem);
+  }
   if (g == 0 && !(ABL & 4)) bar();  // group 1 ran one barrier more
 }
+
 
 int g_pp_group_m = [] {
   const char* e = getenv("ND_GEMM_PP_GM");
@@ -499,15 +552,12 @@ int num_cus_pp() {
 }
 
 int g_pp_variant = 0;  // ablation builds (profiling only, wrong results): nd_gemm_pp_set_variant
-int g_pp_stagger = [] {  // cycles per stagger slot (see the kernel)
-  const char* e = getenv("ND_GEMM_PP_STAGGER");
-  return e ? atoi(e) : 0;
-}();
+
 
 template <int EPI, int HD, int ABL>
 int launch_pp_v(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
                 const PPEpi& ep, hipStream_t s) {
-  const size_t lds = 2 * (size_t)BUF_B;  // 128 KiB
+  const size_t lds = 2 * (size_t)BUF_B + ((ABL & 256) ? 0 : 8 * 4096);  // 128 KiB + 32 KiB C staging
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<EPI, HD, ABL>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return (int)attr;
@@ -515,7 +565,7 @@ int launch_pp_v(const void* A, const void* B, void* C, int M, int N, int K, int6
   const int tiles = ((M + TM - 1) / TM) * ((N + tcols - 1) / tcols);
   const int grid = tiles < num_cus_pp() ? tiles : num_cus_pp();
   hipLaunchKernelGGL((gemm_pp_kernel<EPI, HD, ABL>), dim3(grid), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
-                     (bf16_t*)C, M, N, K, lda, ldb, ldc, ep, g_pp_group_m, g_pp_stagger);
+                     (bf16_t*)C, M, N, K, lda, ldb, ldc, ep, g_pp_group_m);
   ND_LAUNCH_CHECK();
 }
 
@@ -532,6 +582,10 @@ int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_
       case 15: return launch_pp_v<EPI, HD, 15>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       case 16: return launch_pp_v<EPI, HD, 16>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       case 32: return launch_pp_v<EPI, HD, 32>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      case 64: return launch_pp_v<EPI, HD, 64>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      case 128: return launch_pp_v<EPI, HD, 128>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      case 256: return launch_pp_v<EPI, HD, 256>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);  // direct stores
+      case 288: return launch_pp_v<EPI, HD, 288>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);  // direct, plain policy
       default: break;
     }
   }
@@ -595,12 +649,6 @@ ND_API int nd_gemm_pp_dswiglu(const void* A, const void* B, const void* gu, void
 ND_API int nd_gemm_pp_set_variant(int v) {
   const int old = g_pp_variant;
   g_pp_variant = v;
-  return old;
-}
-
-ND_API int nd_gemm_pp_set_stagger(int cycles) {
-  const int old = g_pp_stagger;
-  if (cycles >= 0) g_pp_stagger = cycles;
   return old;
 }
 

@@ -179,7 +179,6 @@ def _declare(L: ctypes.CDLL):
         "nd_gemm_pp_dswiglu": [P, P, P, P, I, I, I, L64, L64, L64, L64, P],
         "nd_gemm_pp_set_group_m": [I],
         "nd_gemm_pp_set_variant": [I],
-        "nd_gemm_pp_set_stagger": [I],
         # weight-gradient GEMM
         "nd_wgrad_splits": [I, I, I],
         "nd_wgrad": [P, P, P, P, I, I, I, L64, L64, L64, P],

@@ -4,7 +4,7 @@ The reference materialises fp32 logits ``[N, V]`` and their gradient (1.05 GB ea
 micro-batch; 33.5 GB at 262k tokens).  Here the N rows are processed in
 chunks; for each chunk:
 
-  1. ``logits = y_c @ W^T``            (hipBLASLt, compute dtype)
+  1. ``logits = y_c @ W^T``            (own GEMM, csrc/gemm_pp.hip; compute dtype)
   2. ``nd_ce_fwd_bwd``                 one HIP kernel, one row per workgroup: online max/sum-exp over V,
                                        per-row loss summed into a device scalar, and the logits
                                        buffer overwritten IN PLACE by ``dlogits = (softmax - onehot) * s``
@@ -28,7 +28,7 @@ import torch
 
 from . import _ext
 from .determinism import deterministic
-from .linear import library_gemm_fence, wgrad_accumulate
+from .linear import mm_nt, wgrad_accumulate
 
 IGNORE_INDEX = -100
 
@@ -63,8 +63,7 @@ class LMHeadCEFn(torch.autograd.Function):
             e = min(n, s + chunk)
             yc, tc = y[s:e], targets[s:e]
             if hip:
-                library_gemm_fence(y.device)
-                logits = torch.mm(yc, w.t())
+                logits = mm_nt(yc, w)  # own projection GEMM (ops/linear.py proj_gemm), hipBLASLt as fallback
                 rows = torch.empty(e - s, dtype=torch.float32, device=y.device) if det else None
                 _ext.check(_ext.lib().nd_ce_fwd_bwd(_ext.ptr(logits), _ext.dtcode(logits), _ext.ptr(tc),
                                                     _ext.ptr(loss_sum), _ext.ptr(scale), e - s, V, IGNORE_INDEX,
@@ -87,7 +86,7 @@ class LMHeadCEFn(torch.autograd.Function):
             # dy rows written in place (a row slice of a contiguous tensor); with wt = W^T the GEMM
             # has the faster K-contiguous operand layout (ops/linear.py)
             if wt is not None and dl.dtype == wt.dtype:
-                torch.mm(dl, wt.t(), out=dy[s:e])
+                mm_nt(dl, wt, out=dy[s:e])
             elif dl.dtype == w.dtype:
                 torch.mm(dl, w, out=dy[s:e])
             else:

@@ -201,11 +201,6 @@ def set_pp_variant(v: int) -> int:
     return int(_ext.lib().nd_gemm_pp_set_variant(int(v)))
 
 
-def set_pp_stagger(cycles: int) -> int:
-    """Cycles per start-stagger slot of the ping-pong kernel's workgroups (0 = off); returns the old."""
-    return int(_ext.lib().nd_gemm_pp_set_stagger(int(cycles)))
-
-
 def set_pp_group_m(g: int) -> int:
     """m-panels per tile group of the ping-pong kernel (XCD L2 locality); returns the old value."""
     return int(_ext.lib().nd_gemm_pp_set_group_m(int(g)))

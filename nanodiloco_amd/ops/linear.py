@@ -157,8 +157,10 @@ def fused_epilogues() -> dict:
     return {"rope": _PROJ["rope"], "mlp": _PROJ["mlp"]}
 
 
-def _pp_ok(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> bool:
-    if _PROJ["gemm"] != "pp" or not a.is_cuda:
+def _pp_ok(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, fused: bool = False) -> bool:
+    """Shape / layout check for the own kernel; plain products also need the 'pp' selection (the
+    fused-epilogue ops exist only on the own kernel and are switched by set_fused_epilogues)."""
+    if (_PROJ["gemm"] != "pp" and not fused) or not a.is_cuda:
         return False
     from .gemm import pp_supported
     return pp_supported(a, b) and (out is None or (out.stride(-1) == 1 and out.stride(0) % 8 == 0
@@ -222,7 +224,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, gw: torch.Tensor, wt: torch.Tensor 
 # Fused epilogues on the own GEMM (csrc/gemm_pp.hip)
 
 def linear_rope_supported(x: torch.Tensor, w: torch.Tensor, wt, hd: int, rope_cols: int) -> bool:
-    return (_PROJ["rope"] and wt is not None and _pp_ok(x, w) and hd in (32, 64) and rope_cols % 64 == 0)
+    return (_PROJ["rope"] and wt is not None and _pp_ok(x, w, fused=True) and hd in (32, 64) and rope_cols % 64 == 0)
 
 
 class LinearRopeFn(torch.autograd.Function):
@@ -253,7 +255,7 @@ def linear_rope(x, w, gw, wt, cos, sin, T: int, hd: int, rope_cols: int) -> torc
 
 def mlp_fused_supported(y: torch.Tensor, w_gu: torch.Tensor, wt_gu, w_down: torch.Tensor, wt_down) -> bool:
     F = w_gu.shape[0] // 2
-    return (_PROJ["mlp"] and wt_gu is not None and wt_down is not None and _pp_ok(y, w_gu) and F % 8 == 0
+    return (_PROJ["mlp"] and wt_gu is not None and wt_down is not None and _pp_ok(y, w_gu, fused=True) and F % 8 == 0
             and w_down.shape[1] == F and w_down.shape[0] % 8 == 0)
 
 

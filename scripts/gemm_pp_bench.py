@@ -120,14 +120,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--no-old", action="store_true", help="skip the round-2 own kernel")
-    ap.add_argument("--stagger", default="", help="comma list of stagger cycles per slot to A/B (G.set_pp_stagger)")
+    ap.add_argument("--gms", default="", help="comma list of tile-group sizes (G.set_pp_group_m) to A/B")
     ap.add_argument("--ablate", default="", help="comma list of ablation variants (G.set_pp_variant) to time "
                                                  "on the qkv-fwd / gu-dgrad / lm-dgrad shapes instead")
     a = ap.parse_args()
     ops.set_backend("hip")
-    if a.ablate or a.stagger:
+    if a.ablate or a.gms:
         vs = [int(v) for v in a.ablate.split(",")] if a.ablate else []
-        sts = [int(v) for v in a.stagger.split(",")] if a.stagger else []
+        gms = [int(v) for v in a.gms.split(",")] if a.gms else []
         res = {}
         shapes = {"qkv fwd": (65536, 3072, 1024), "gu dgrad": (65536, 1024, 5376), "o fwd": (65536, 1024, 1024),
                   "lm logits": (65536, 32000, 1024)}
@@ -143,13 +143,13 @@ def main():
                     G.set_pp_variant(v)
                     res.setdefault((nm, v), []).append(timed(lambda: G.gemm_pp(x, w, out)))
                 G.set_pp_variant(0)
-                for st in sts:
-                    old = G.set_pp_stagger(st)
-                    res.setdefault((nm, f"st{st}"), []).append(timed(lambda: G.gemm_pp(x, w, out)))
-                    G.set_pp_stagger(old)
+                for gm in gms:
+                    old = G.set_pp_group_m(gm)
+                    res.setdefault((nm, f"gm{gm}"), []).append(timed(lambda: G.gemm_pp(x, w, out)))
+                    G.set_pp_group_m(old)
         for nm, (x, w, out, fl) in ops_.items():
             line = f"{nm:9s}"
-            for arm in ["blas"] + vs + [f"st{st}" for st in sts]:
+            for arm in ["blas"] + vs + [f"gm{gm}" for gm in gms]:
                 t = sorted(res[(nm, arm)])[len(res[(nm, arm)]) // 2]
                 line += f" | {arm}: {t:7.1f} us {fl / t / 1e6:5.0f} TF"
             print(line, flush=True)
