@@ -127,12 +127,15 @@ def wgrad_accumulate(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor):
     gw.add_(torch.mm(dy.t(), x).float())
 
 
-# ---- which GEMM runs the projections' forward / input-gradient products (and the lm head's)
-#   "pp"   own ping-pong MFMA kernel (csrc/gemm_pp.hip; ops.gemm.gemm_pp) -- the GPU default
-#   "blas" hipBLASLt through torch.mm (A/B runs; shapes the own kernel does not take always use it)
-# plus the epilogue fusions that only exist on the own kernel (RoPE into the q|k|v projection,
-# SwiGLU into the gate|up projection, the SwiGLU backward into the down projection's dgrad)
-_PROJ = {"gemm": "pp", "rope": True, "mlp": True}
+# ---- which GEMM runs the PLAIN projection products (forward / input gradient, lm head)
+#   "blas" hipBLASLt through torch.mm -- the default: the own kernel reaches 0.94-1.01x of it per
+#          shape (profiles/r3_gemm_pp.md) and the step is 1.5 % faster this way
+#   "pp"   own ping-pong MFMA kernel (csrc/gemm_pp.hip; ops.gemm.gemm_pp) for every projection
+# The FUSED products always run on the own kernel (they exist only there): RoPE in the q|k|v
+# projection's epilogue, SwiGLU in the gate|up projection's, the SwiGLU backward in the down
+# projection's dgrad -- on by default (+0.8 % end to end over hipBLASLt + separate kernels,
+# +2.3 % on the own kernel; profiles/r3_gemm_pp.md).
+_PROJ = {"gemm": "blas", "rope": True, "mlp": True}
 
 
 def set_proj_gemm(name: str) -> None:
@@ -168,7 +171,8 @@ def _pp_ok(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, fused: bo
 
 
 def mm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
-    """a[M, K] . b[N, K]^T on the selected projection GEMM (own kernel when it takes the shape)."""
+    """a[M, K] . b[N, K]^T on the selected projection GEMM (the own kernel when 'pp' is selected and
+    it takes the shape; hipBLASLt otherwise)."""
     if _pp_ok(a, b, out):
         from .gemm import gemm_pp
         return gemm_pp(a, b, out)

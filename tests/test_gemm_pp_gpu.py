@@ -165,14 +165,39 @@ def test_fused_mlp_and_rope_match_unfused_chain():
 
 
 def test_proj_gemm_switch_routes_to_own_kernel():
-    """With the default 'pp' projection GEMM the model's linears run gemm_pp (bitwise equal to a
-    direct call), and 'blas' falls back to torch.mm."""
+    """'pp' routes the plain projection products to gemm_pp (bitwise equal to a direct call); the
+    default 'blas' uses torch.mm (hipBLASLt)."""
     x = torch.randn(1024, 512, device=DEV).bfloat16()
     w = (torch.randn(768, 512, device=DEV) * 0.05).bfloat16()
-    assert ops.proj_gemm() == "pp"
-    assert torch.equal(ops.mm_nt(x, w), G.gemm_pp(x, w))
-    ops.set_proj_gemm("blas")
+    assert ops.proj_gemm() == "blas"
+    assert torch.equal(ops.mm_nt(x, w), torch.mm(x, w.t()))
+    ops.set_proj_gemm("pp")
     try:
-        assert torch.equal(ops.mm_nt(x, w), torch.mm(x, w.t()))
+        assert torch.equal(ops.mm_nt(x, w), G.gemm_pp(x, w))
     finally:
-        ops.set_proj_gemm("pp")
+        ops.set_proj_gemm("blas")
+
+
+@pytest.mark.parametrize("proj", ["blas", "pp"])
+def test_model_step_fused_vs_unfused(proj):
+    """A 2-layer Llama forward+backward: the fused-epilogue path (default) and the unfused path give
+    the same loss and gradients to bf16 tolerance, with either plain-GEMM backend."""
+    from nanodiloco_amd.config import LlamaConfig
+    from nanodiloco_amd.models import LlamaForCausalLM
+    cfg = LlamaConfig(vocab_size=4096, hidden_size=256, intermediate_size=704, num_hidden_layers=2,
+                      num_attention_heads=4, num_key_value_heads=4, max_position_embeddings=512)
+    ids = torch.randint(0, cfg.vocab_size, (4, 512), device=DEV)
+    out = {}
+    ops.set_proj_gemm(proj)
+    try:
+        for fused in (True, False):
+            ops.set_fused_epilogues(rope=fused, mlp=fused)
+            m = LlamaForCausalLM(cfg, DEV, torch.bfloat16).init_weights(3)
+            loss = m(ids, labels=ids).loss
+            loss.backward()
+            out[fused] = (loss.detach().float(), m.store.grad.clone())
+    finally:
+        ops.set_fused_epilogues(rope=True, mlp=True)
+        ops.set_proj_gemm("blas")
+    assert abs(out[True][0].item() - out[False][0].item()) < 2e-3 * abs(out[False][0].item())
+    assert rel(out[True][1], out[False][1]) < 2e-2
