@@ -166,21 +166,37 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
     if constexpr (EPI == PP_STORE || EPI == PP_ROPE) {
       const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
       constexpr int HALFD = HD / 2;
+      // RoPE tables: the loads of four row blocks are issued together (64 VGPRs -- the next K-tile's
+      // fragment registers are free during the epilogue), so the epilogue waits for table data twice
+      // per tile instead of once per row block (each wait also drains the LDS-DMA issued before it)
+      constexpr int NJ = EPI == PP_ROPE ? (HALFD + 15) / 16 : 1;
+      float4 ctab[4][NJ], stab[4][NJ];
 #pragma unroll
       for (int a = 0; a < 8; ++a) {
         const int mr = g * 128 + a * 16 + r16;  // row inside the tile
+        if constexpr (EPI == PP_ROPE) {
+          if ((a & 3) == 0) {
+#pragma unroll
+            for (int aa = 0; aa < 4; ++aa) {
+              const int t = (m0 + mr + aa * 16) % ep.T;
+#pragma unroll
+              for (int j = 0; j < NJ; ++j) {
+                ctab[aa][j] = *reinterpret_cast<const float4*>(ep.cosT + (int64_t)t * HD + j * 16 + 4 * q);
+                stab[aa][j] = *reinterpret_cast<const float4*>(ep.sinT + (int64_t)t * HD + j * 16 + 4 * q);
+              }
+            }
+          }
+        }
         f32x4 v[4] = {acc[a][0], acc[a][1], acc[a][2], acc[a][3]};
         if constexpr (EPI == PP_ROPE) {
           // the wave's 64 columns are one 64-wide head (or two 32-wide ones): column block b pairs
           // with b + HD / 32 in the same lane; v columns (>= rope_cols) pass through
           const bool rot = n0 + wn * 64 < ep.rope_cols;
-          const int t = (m0 + mr) % ep.T;
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
             if (((b * 16) % HD) >= HALFD) continue;
-            const int p = b + HALFD / 16, i = (b * 16) % HD + 4 * q;
-            const float4 c = *reinterpret_cast<const float4*>(ep.cosT + (int64_t)t * HD + i);
-            const float4 s = *reinterpret_cast<const float4*>(ep.sinT + (int64_t)t * HD + i);
+            const int p = b + HALFD / 16, j = ((b * 16) % HD) / 16;
+            const float4 c = ctab[a & 3][j], s = stab[a & 3][j];
             const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {

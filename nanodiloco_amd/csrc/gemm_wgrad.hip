@@ -620,6 +620,184 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
   }
 }
 
+// =====================================================================================================
+// Ping-pong weight-gradient kernel (round 3, the default for K % 64 == 0): the pairing of
+// csrc/gemm_pp.hip applied to C (+)= A^T B.  8 waves, 256 x 256 tile; group g = w / 4 owns output rows
+// m 128 g .. + 127, wave w % 4 the 64 columns n 64 (w % 4) .. + 63 (8 x 4 v_mfma_f32_16x16x32_bf16
+// accumulators, 128 VGPRs, + one K-tile of fragments, 96 VGPRs: 2 waves / SIMD).  Each 64-token K-tile
+// is a LOAD phase (all 48 transposing fragment reads of the K-tile + this group's LDS-DMA pieces) and a
+// COMPUTE phase (64 MFMAs), group 1 one barrier behind group 0, so the two waves of a SIMD alternate
+// matrix work and loads.  The LDS image holds the operands as they lie in memory ([k][m] / [k][n]
+// half-tiles of 64 rows x 256 B, 16-B chunk index ^ f(row), f = ((row & 3) << 2) ^ (((row >> 3) & 1) << 1):
+// the 32 lanes of one ds_read_b64_tr_b16 read rows q and q + 8 (q = 0..3) at one 32-B column pair
+// -> 8 distinct 32-B bank segments).  DMA ownership and counted waits are those of gemm_pp_kernel:
+// group 0 stages B (both halves) of K-tile s + 1 in LOAD(s) and retires it at the end of COMPUTE(s);
+// group 1 stages A1 of s + 1 and A0 of s + 2, retiring A0(s + 1) at the end of LOAD(s) and A1(s + 1)
+// at the end of COMPUTE(s).  One (tile, K-split) per workgroup; split-K slabs as wgrad_dma_kernel.
+namespace {
+constexpr uint32_t WPP_HALF_B = 64 * 128 * 2;  // [64 k][128 cols] bf16
+constexpr uint32_t WPP_BUF_B = 4 * WPP_HALF_B;  // A0 A1 B0 B1 = 64 KiB
+
+__device__ __forceinline__ uint32_t wpp_off(int row, int ch) {
+  return (uint32_t)(row * 256 + ((ch ^ (((row & 3) << 2) ^ (((row >> 3) & 1) << 1))) << 4));
+}
+// 16x16x32 operand, the column (m or n) on the lane: lane l -> column c0 + (l & 15), k = kb + 8 (l >> 4) + j
+__device__ __forceinline__ bf16x8 wpp_frag(const char* half, int kb, int c0, int lane) {
+  const int gg = lane >> 4, i = lane & 15;
+  const int row = kb + 8 * gg + (i >> 2), col = c0 + 4 * (i & 3);
+  const char* p = half + wpp_off(row, col >> 3) + (col & 7) * 2;
+  const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((sv4 __attribute__((address_space(3)))*)(p));
+  const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((sv4 __attribute__((address_space(3)))*)(p + 1024));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+__device__ __forceinline__ f32x4 wpp_mma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bfv8, a), __builtin_bit_cast(bfv8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wpp_rsrc(const void* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
+                                           (int)(bytes > 0 ? (bytes < 0x7ffffffe ? bytes : 0x7ffffffe) : 0), 0x00020000);
+}
+__device__ __forceinline__ void wpp_dma(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void wpp_bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+template <int N> __device__ __forceinline__ void wpp_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+__device__ __forceinline__ void wpp_vmn(int n) {  // n in {0, 4, 8}
+  if (n >= 8) wpp_vm<8>();
+  else if (n >= 4) wpp_vm<4>();
+  else wpp_vm<0>();
+}
+}  // namespace
+
+__global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                          float* __restrict__ C, float* __restrict__ slab, int M, int N,
+                                                          int K, int64_t lda, int64_t ldb, int64_t ldc, int S, int kchunk) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem_bf[];
+  char* smem = reinterpret_cast<char*>(smem_bf);
+  const int tn_count = (N + 255) / 256;
+  const int tiles = ((M + 255) / 256) * tn_count;
+  const int id = xcd_remap(blockIdx.x, tiles * S);
+  const int split = id / tiles, tile = id % tiles;
+  const int m0 = (tile / tn_count) * 256, n0 = (tile % tn_count) * 256;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int nk = (kend - kbeg) / 64;  // host: K % 64 == 0, kchunk % 64 == 0, every split non-empty
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = w >> 2, wn = w & 3;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+
+  // DMA: piece q of this wave = half-tile rows 4 j .. 4 j + 3 (j = wn + 4 q); lane -> row 4 j + lane / 16,
+  // physical chunk lane & 15 <- logical chunk (lane & 15) ^ f(row), f independent of q
+  const int64_t ld = g == 0 ? ldb : lda;
+  const int fsw = ((lane >> 4) << 2) ^ (((wn >> 1) & 1) << 1);
+  uint32_t voff[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = 4 * (wn + 4 * q) + (lane >> 4);
+    voff[q] = (uint32_t)(((int64_t)row * ld + (((lane & 15) ^ fsw) << 3)) * 2);
+  }
+  // half h of operand (g == 0: B columns n0 + 128 h .., g == 1: A columns m0 + 128 h ..) of K-tile kt
+  auto stage = [&](int kt, int h) __attribute__((always_inline)) {
+    const int64_t e0 = (int64_t)(kbeg + 64 * kt) * ld + (g == 0 ? n0 : m0) + 128 * h;
+    const auto r = wpp_rsrc((g == 0 ? B : A) + e0, ((int64_t)K * ld - e0) * 2);
+    const uint32_t dst = lds0 + (uint32_t)(kt & 1) * WPP_BUF_B + (uint32_t)(g == 0 ? 2 + h : h) * WPP_HALF_B +
+                         (uint32_t)wn * 1024u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wpp_dma(r, voff[q], dst + (uint32_t)q * 4096u);
+  };
+  bf16x8 fa[8][2], fb[4][2];
+  auto load_frags = [&](int kt) __attribute__((always_inline)) {
+    const char* base = smem + (kt & 1) * WPP_BUF_B;
+    const char* ah = base + g * WPP_HALF_B;
+    const char* bh = base + (2 + (wn >> 1)) * WPP_HALF_B;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) fb[b][ks] = wpp_frag(bh, 32 * ks, (wn & 1) * 64 + 16 * b, lane);
+#pragma unroll
+      for (int a = 0; a < 8; ++a) fa[a][ks] = wpp_frag(ah, 32 * ks, 16 * a, lane);
+    }
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-tile 0 and A0 of K-tile 1, drained; group 1 one barrier behind
+  if (g == 0) {
+    stage(0, 0);
+    stage(0, 1);
+  } else {
+    stage(0, 0);
+    stage(0, 1);
+    if (nk > 1) stage(1, 0);
+  }
+  wpp_vm<0>();
+  wpp_bar();
+  if (g == 1) wpp_bar();
+  for (int s = 0; s < nk; ++s) {
+    const bool more1 = s + 1 < nk, more2 = s + 2 < nk;
+    // ================= LOAD(s)
+    if (g == 0) {
+      if (more1) {
+        stage(s + 1, 0);
+        stage(s + 1, 1);
+      }
+    } else {
+      if (more1) stage(s + 1, 1);  // A1(s + 1)
+      if (more2) stage(s + 2, 0);  // A0(s + 2)
+    }
+    load_frags(s);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (g == 1) wpp_vmn((more1 ? 4 : 0) + (more2 ? 4 : 0));  // A0(s + 1) landed
+    wpp_bar();
+    // ================= COMPUTE(s)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = wpp_mma(fa[a][ks], fb[b][ks], acc[a][b]);
+    __builtin_amdgcn_s_setprio(0);
+    if (g == 0) wpp_vm<0>();            // B(s + 1) landed
+    else wpp_vmn(more2 ? 4 : 0);        // A1(s + 1) landed
+    wpp_bar();
+  }
+  // epilogue: acc[a][b] lane l reg r = C[m0 + 128 g + 16 a + 4 (l >> 4) + r][n0 + 64 wn + 16 b + (l & 15)]
+  float* out = S == 1 ? C : slab + (int64_t)split * M * N;
+  const int64_t ldo = S == 1 ? ldc : N;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int n = n0 + wn * 64 + b * 16 + (lane & 15);
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + g * 128 + a * 16 + 4 * (lane >> 4) + r;
+        if (m < M) {
+          float* p = out + (int64_t)m * ldo + n;
+          if (S == 1) *p += acc[a][b][r];
+          else *p = acc[a][b][r];
+        }
+      }
+    }
+  if (g == 0) wpp_bar();  // group 1 ran one barrier more
+}
+
 static int splits_for(int tiles, int K, int bk, int target) {
   int S = target / tiles;
   if (S < 1) S = 1;
@@ -677,7 +855,18 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
   // the sched_group_barrier interleave (MFMA / 2 transposing reads) is opt-in ("dmas"): measured
   // 4-13 % SLOWER per kernel than the compiler's own schedule at 32k and 64k tokens, -1.7 % e2e
   const bool sched = ev && ev[0] == 'd' && ev[3] == 's';
-  if (large && variant == 5 && M >= 8 && N >= 8 && K % BK3 == 0) {  // "4w": 4-wave, AGPR-pinned accumulators
+  const bool pp = large && M >= 8 && N >= 8 && K % 64 == 0 && (int64_t)64 * (lda > ldb ? lda : ldb) * 2 < (1ll << 31) &&
+                 !(ev && (ev[0] == 'd' || ev[0] == 'r' || ev[0] == 'n' || ev[0] == '4'));
+  if (pp) {  // default: ping-pong kernel (ND_WGRAD_VARIANT=dma0 / reg / ... select the older kernels)
+    const int kchunk = fit_kchunk(K, &S, 64);
+    const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+    const size_t lds = 2 * (size_t)WPP_BUF_B;  // 128 KiB
+    static const hipError_t attrp = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (attrp != hipSuccess) return (int)attrp;
+    hipLaunchKernelGGL(wgrad_pp_kernel, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B, C, slab,
+                       M, N, K, lda, ldb, ldc, S, kchunk);
+  } else if (large && variant == 5 && M >= 8 && N >= 8 && K % BK3 == 0) {  // "4w": 4-wave, AGPR-pinned accumulators
     const int kchunk = fit_kchunk(K, &S, BK3);
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB

@@ -12,6 +12,8 @@ def main(path, top=25, steps=None):
         name = r["Name"]
         if name.startswith("void "):
             name = name[5:]
+        if name.startswith("(anonymous namespace)::"):
+            name = name[len("(anonymous namespace)::"):]
         name = name.split("(")[0][:90]
         print(f"| `{name}` | {r['Calls']} | {float(r['TotalDurationNs'])/1e6:.1f} | "
               f"{float(r['AverageNs'])/1e3:.1f} | {float(r['Percentage']):.1f} |")

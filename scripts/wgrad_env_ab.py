@@ -2,7 +2,7 @@
 """In-process interleaved A/B of weight-gradient kernel variants (ND_WGRAD_VARIANT is read per call)
 on the Llama-150M wgrad shapes at 65,536 tokens (lm head: 16,384-token chunks).
 
-    python scripts/wgrad_env_ab.py --variants ,stg --rounds 7
+    python scripts/wgrad_env_ab.py --variants ,dma0 --rounds 7   (default = ping-pong kernel, dma0 = round-2 kernel)
 """
 import argparse
 import os
@@ -28,7 +28,7 @@ def timed(fn, iters=5):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default=",stg")
+    ap.add_argument("--variants", default=",dma0")
     ap.add_argument("--rounds", type=int, default=7)
     a = ap.parse_args()
     vs = a.variants.split(",")

@@ -205,10 +205,14 @@ def test_dgrad_transposed_weights(graphed):
     batches = [torch.randint(0, 1000, (4, 256), device="cuda") for _ in range(7)]
     prev = ops.dgrad_transposed_enabled()
     try:
+        # the fused-epilogue GEMMs need the W^T copies (they are off without them), so compare the two
+        # dgrad layouts with the fusions off in both runs: this test is about the layouts
+        ops.set_fused_epilogues(rope=False, mlp=False)
         ops.set_dgrad_transposed(False)
         l0, g0, p0 = _trajectory(cfg, batches, graphed)
         ops.set_dgrad_transposed(True)
         l1, g1, p1 = _trajectory(cfg, batches, graphed)
+        ops.set_fused_epilogues(rope=True, mlp=True)
         # freshness of the copies after 3 optimizer steps + one more micro-batch
         m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16).init_weights(5)
         opt = FlatAdamW(m.store, lr=1e-3)
@@ -232,9 +236,30 @@ def test_dgrad_transposed_weights(graphed):
             assert torch.equal(wt, w.t()), key
     finally:
         ops.set_dgrad_transposed(prev)
+        ops.set_fused_epilogues(rope=True, mlp=True)
     assert ((l1 - l0).abs() / l0.abs()).max().item() < 1e-3, (l0, l1)
     assert _rel(g1, g0) < 2e-2
     assert _rel(p1, p0) < 5e-4
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_fused_epilogue_trajectory(graphed):
+    """7 optimizer steps with the fused RoPE / SwiGLU / SwiGLU-backward GEMM epilogues vs the unfused
+    op chain: the fused path rounds once where the chain rounds twice (RoPE on the fp32 accumulator,
+    d(act) never rounded to bf16), so the trajectories agree to bf16 rounding, not bitwise."""
+    ops.set_backend("hip")
+    cfg = LlamaConfig.from_dict(_CFG_SMALL)
+    batches = [torch.randint(0, 1000, (4, 256), device="cuda") for _ in range(7)]
+    try:
+        ops.set_fused_epilogues(rope=False, mlp=False)
+        l0, g0, p0 = _trajectory(cfg, batches, graphed)
+        ops.set_fused_epilogues(rope=True, mlp=True)
+        l1, g1, p1 = _trajectory(cfg, batches, graphed)
+    finally:
+        ops.set_fused_epilogues(rope=True, mlp=True)
+    assert ((l1 - l0).abs() / l0.abs()).max().item() < 2e-3, (l0, l1)
+    assert _rel(g1, g0) < 5e-2
+    assert _rel(p1, p0) < 5e-3
 
 
 def test_trainer_auto_hip_graph_small_model(tmp_path):
