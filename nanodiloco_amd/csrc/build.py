@@ -82,6 +82,12 @@ def build(force: bool = False, jobs: int = 0, save_temps: bool = False, verbose:
         objs.append(o)
         if force or _stale([s] + sorted(headers), o, " ".join(flags + FILE_FLAGS.get(os.path.basename(s), []))):
             todo.append((s, o))
+    # objects of sources that no longer exist (renamed / removed kernels) are deleted, never linked
+    for o in glob.glob(os.path.join(OBJ_DIR, "*.hip.o")):
+        if o not in objs:
+            for f in (o, o + ".sha256"):
+                if os.path.exists(f):
+                    os.remove(f)
     jobs = jobs or min(8, os.cpu_count() or 4)
 
     def comp(so):

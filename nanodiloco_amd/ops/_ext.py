@@ -164,14 +164,9 @@ def _declare(L: ctypes.CDLL):
         "nd_fp8_cast": [P, I, L64, P, P, I, P, I, P],
         "nd_fp8_cast_t": [P, I, I, I, L64, P, P, P, I, P, I, P],
         # projection GEMMs (C = A B^T) and their fused epilogues
-        "nd_gemm_nt": [P, P, P, I, I, I, L64, L64, L64, P],
         "nd_gemm_nt_f8": [P, P, P, I, I, I, L64, L64, L64, I, I, P, P, P],
-        "nd_gemm_set_variant": [I],
         "nd_gemm_set_group_m": [I],
         "nd_gemm_set_f8_variant": [I],
-        "nd_gemm_nt_rope": [P, P, P, I, I, I, L64, L64, L64, P, P, I, I, I, P],
-        "nd_gemm_nt_swiglu": [P, P, P, P, I, I, I, L64, L64, L64, L64, P],
-        "nd_gemm_nt_dswiglu": [P, P, P, P, I, I, I, L64, L64, L64, L64, P],
         # ping-pong projection GEMMs (csrc/gemm_pp.hip)
         "nd_gemm_pp": [P, P, P, I, I, I, L64, L64, L64, P],
         "nd_gemm_pp_rope": [P, P, P, I, I, I, L64, L64, L64, P, P, I, I, I, P],

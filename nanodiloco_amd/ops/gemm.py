@@ -1,21 +1,16 @@
-"""Own MFMA GEMMs (csrc/gemm.hip, csrc/gemm_wgrad.hip).
+"""Own MFMA GEMMs (csrc/gemm_pp.hip, csrc/gemm_wgrad.hip, csrc/gemm_f8.hip).
 
-* ``gemm_nt``        C[M, N] = A[M, K] . B[N, K]^T -- every projection forward and (with the W^T copies
-                     of ops/linear.py) every input-gradient GEMM, the lm-head logits and dgrad.
-* ``gemm_nt_rope``   the q|k|v projection with RoPE applied to q and k in the epilogue.
-* ``gemm_nt_swiglu`` the gate|up projection writing gu AND act = silu(gate) * up.
-* ``gemm_nt_dswiglu``the down projection's input gradient fused with the SwiGLU backward: writes
-                     d(gate|up) straight from the accumulator (d(act) never stored).
-* ``wgrad``          ``gW[M, N] (fp32) += dY[K, M]^T @ X[K, N]`` -- the token-reduction layout hipBLASLt
-                     runs at 330-900 TF/s on the Llama-150M shapes: both operands are staged through LDS
-                     as they lie in memory and fragments formed with transposing LDS reads, with a
-                     deterministic split-K for the small outputs.
-
-Where each kernel runs: ``wgrad`` is the weight gradient of every projection on the default path
-(ops/linear.py).  The NT kernels are called by ``ops.linear`` / ``ops.cross_entropy`` only when
-their switches select them (``ops.linear.set_own_gemm`` and the fused-epilogue switches, see
-ops/linear.py); ``set_gemm_backend("blas")`` disables them for A/B runs.  Shapes outside
-``nt_supported`` (K % 64, N % 4, alignment) always use hipBLASLt (``torch.mm``).
+* ``gemm_pp``          C[M, N] = A[M, K] . B[N, K]^T on the ping-pong kernel (two waves per SIMD in
+                       opposite load / MFMA phases) -- the plain projection products when
+                       ``ops.linear.set_proj_gemm("pp")`` is selected (default: hipBLASLt, which it
+                       reaches 0.94-1.01x of, profiles/r3_gemm_pp.md).
+* ``gemm_pp_rope``     the q|k|v projection with RoPE on q and k in the epilogue      } on the default
+* ``gemm_pp_swiglu``   the gate|up projection writing gu AND act = silu(gate) * up    } path (ops/linear.py
+* ``gemm_pp_dswiglu``  the down projection's dgrad fused with the SwiGLU backward     } LinearRopeFn, MLPFn)
+* ``gemm_nt_f8``       fp8 x fp8 -> bf16 (``--fp8 --fp8-gemm hip``)
+* ``wgrad``            ``gW[M, N] (fp32) += dY[K, M]^T @ X[K, N]`` -- the weight gradient of every projection
+                       (default path): both operands staged through LDS as they lie in memory, fragments
+                       by transposing LDS reads, ping-pong pairing, deterministic split-K.
 """
 from __future__ import annotations
 
@@ -28,7 +23,7 @@ _GEMM = {"backend": "hip"}
 
 
 def set_gemm_backend(name: str) -> None:
-    """'hip': own MFMA kernels for the projection GEMMs (default); 'blas': hipBLASLt (A/B)."""
+    """'hip': the own kernels may run (default); 'blas': ``pp_supported`` refuses every shape (A/B)."""
     if name not in ("hip", "blas"):
         raise ValueError(name)
     _GEMM["backend"] = name
@@ -42,40 +37,14 @@ def _aligned(t: torch.Tensor) -> bool:
     return t.data_ptr() % 16 == 0 and t.stride(-1) == 1 and t.stride(0) % 8 == 0
 
 
-def nt_supported(a: torch.Tensor, b: torch.Tensor) -> bool:
-    """Can ``gemm_nt(a, b)`` (C = a . b^T) run on the own kernel?"""
-    return (_GEMM["backend"] == "hip" and a.is_cuda and _ext.get_backend() != "torch"
-            and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
-            and a.shape[1] == b.shape[1] and a.shape[1] % 64 == 0 and b.shape[0] % 4 == 0
-            and _aligned(a) and _aligned(b))
-
-
-def set_gemm_variant(v: int) -> int:
-    """Schedule variant of the own NT GEMM (csrc/gemm.hip ``g_variant``; A/B runs); returns the old one."""
-    return int(_ext.lib().nd_gemm_set_variant(int(v)))
-
-
 def set_gemm_f8_variant(v: int) -> int:
-    """fp8 GEMM schedule (csrc/gemm.hip g_f8_variant, A/B); returns the previous one."""
+    """fp8 GEMM schedule (csrc/gemm_f8.hip g_f8_variant, A/B); returns the previous one."""
     return _ext.lib().nd_gemm_set_f8_variant(int(v))
 
 
 def set_gemm_group_m(g: int) -> int:
-    """Tile grouping (m-panels per group) of the 4-wave GEMM variants; 0/1 = row-major tiles."""
+    """Tile grouping (m-panels per group) of the fp8 GEMM; 0/1 = row-major tiles."""
     return int(_ext.lib().nd_gemm_set_group_m(int(g)))
-
-
-def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, variant: int = None) -> torch.Tensor:
-    """out[M, N] = a[M, K] . b[N, K]^T (bf16, fp32 accumulate)."""
-    if variant is not None:
-        set_gemm_variant(variant)
-    M, K = a.shape
-    N = b.shape[0]
-    if out is None:
-        out = torch.empty(M, N, dtype=a.dtype, device=a.device)
-    _ext.check(_ext.lib().nd_gemm_nt(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0), b.stride(0),
-                                     out.stride(0), _ext.stream_ptr(a.device)), "nd_gemm_nt")
-    return out
 
 
 _F8_FMT = {torch.float8_e4m3fn: 0, torch.float8_e5m2: 1}
@@ -102,41 +71,6 @@ def gemm_nt_f8(a: torch.Tensor, b: torch.Tensor, scale_a: torch.Tensor, scale_b:
                                         out.stride(0), _F8_FMT[a.dtype], _F8_FMT[b.dtype], _ext.ptr(scale_a),
                                         _ext.ptr(scale_b), _ext.stream_ptr(a.device)), "nd_gemm_nt_f8")
     return out
-
-
-def gemm_nt_rope(a, b, cos, sin, T: int, hd: int, rope_cols: int, out=None) -> torch.Tensor:
-    """q|k|v projection with RoPE on the first ``rope_cols`` columns (tokens are rows, t = row % T)."""
-    M, K = a.shape
-    N = b.shape[0]
-    if out is None:
-        out = torch.empty(M, N, dtype=a.dtype, device=a.device)
-    _ext.check(_ext.lib().nd_gemm_nt_rope(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0), b.stride(0),
-                                          out.stride(0), _ext.ptr(cos), _ext.ptr(sin), T, hd, rope_cols,
-                                          _ext.stream_ptr(a.device)), "nd_gemm_nt_rope")
-    return out
-
-
-def gemm_nt_swiglu(a, w_gu, gu_out=None, act_out=None):
-    """(gu, act): gu = a . w_gu^T ([M, 2F]), act = silu(gu[:, :F]) * gu[:, F:] ([M, F])."""
-    M, K = a.shape
-    F = w_gu.shape[0] // 2
-    gu = gu_out if gu_out is not None else torch.empty(M, 2 * F, dtype=a.dtype, device=a.device)
-    act = act_out if act_out is not None else torch.empty(M, F, dtype=a.dtype, device=a.device)
-    _ext.check(_ext.lib().nd_gemm_nt_swiglu(_ext.ptr(a), _ext.ptr(w_gu), _ext.ptr(gu), _ext.ptr(act), M, F, K,
-                                            a.stride(0), w_gu.stride(0), gu.stride(0), act.stride(0),
-                                            _ext.stream_ptr(a.device)), "nd_gemm_nt_swiglu")
-    return gu, act
-
-
-def gemm_nt_dswiglu(dy, w_down_t, gu, dgu_out=None):
-    """d(gate|up) [M, 2F] of act = silu(gate) * up, where d(act) = dy . w_down_t^T (never stored)."""
-    M, K = dy.shape
-    F = w_down_t.shape[0]
-    dgu = dgu_out if dgu_out is not None else torch.empty_like(gu)
-    _ext.check(_ext.lib().nd_gemm_nt_dswiglu(_ext.ptr(dy), _ext.ptr(w_down_t), _ext.ptr(gu), _ext.ptr(dgu), M, F, K,
-                                             dy.stride(0), w_down_t.stride(0), gu.stride(0), dgu.stride(0),
-                                             _ext.stream_ptr(dy.device)), "nd_gemm_nt_dswiglu")
-    return dgu
 
 
 # ---- ping-pong kernels (csrc/gemm_pp.hip): two waves per SIMD in opposite LOAD / COMPUTE phases

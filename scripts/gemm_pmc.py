@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A few launches of one projection shape on the own NT GEMM and on hipBLASLt (for rocprofv3 --pmc).
+"""A few launches of one projection shape on the own ping-pong GEMM and on hipBLASLt (for rocprofv3 --pmc).
 
     python scripts/gemm_pmc.py [--m 65536 --n 3072 --k 1024] [--iters 10]
 """
@@ -18,8 +18,7 @@ ap.add_argument("--m", type=int, default=65536)
 ap.add_argument("--n", type=int, default=3072)
 ap.add_argument("--k", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=10)
-ap.add_argument("--variants", default="")
-ap.add_argument("--pp", action="store_true", help="the ping-pong kernel (csrc/gemm_pp.hip) instead of gemm_nt")
+ap.add_argument("--variants", default="", help="ping-pong ablation variants (G.set_pp_variant)")
 a = ap.parse_args()
 ops.set_backend("hip")
 x = (torch.rand(a.m, a.k, device="cuda") * 2 - 1).bfloat16()
@@ -28,10 +27,10 @@ out = torch.empty(a.m, a.n, device="cuda", dtype=torch.bfloat16)
 vs = [int(v) for v in a.variants.split(",")] if a.variants else [None]
 for _ in range(a.iters):
     for v in vs:
-        if a.pp:
-            G.gemm_pp(x, w, out)
-        else:
-            G.gemm_nt(x, w, out, variant=v) if v is not None else G.gemm_nt(x, w, out)
+        if v is not None:
+            G.set_pp_variant(v)
+        G.gemm_pp(x, w, out)
+        G.set_pp_variant(0)
     torch.mm(x, w.t(), out=out)
 torch.cuda.synchronize()
 print("done")

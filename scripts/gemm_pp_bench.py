@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Ping-pong GEMM (csrc/gemm_pp.hip): numerics against an fp32 torch reference, then an interleaved
-in-process timing A/B against hipBLASLt (torch.mm) and the round-2 own kernel (gemm_nt) on the
+in-process timing A/B against hipBLASLt (torch.mm) on the
 Llama-150M / 1B projection shapes, random operands.
 
     python scripts/gemm_pp_bench.py [--tokens 65536] [--model 150m|1b] [--rounds 5] [--check-only]
@@ -119,7 +119,6 @@ def main():
     ap.add_argument("--model", default="150m")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--check-only", action="store_true")
-    ap.add_argument("--no-old", action="store_true", help="skip the round-2 own kernel")
     ap.add_argument("--gms", default="", help="comma list of tile-group sizes (G.set_pp_group_m) to A/B")
     ap.add_argument("--ablate", default="", help="comma list of ablation variants (G.set_pp_variant) to time "
                                                  "on the qkv-fwd / gu-dgrad / lm-dgrad shapes instead")
@@ -168,8 +167,6 @@ def main():
         x, w = r(m, k), r(n, k) * 0.05
         out = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
         arms = {"blas": lambda: torch.mm(x, w.t(), out=out), "pp": lambda: G.gemm_pp(x, w, out)}
-        if not a.no_old:
-            arms["nt"] = lambda: G.gemm_nt(x, w, out)
         cases.append((name, 2.0 * m * n * k, arms))
 
     plain("qkv fwd", M, qkv_n, d)
