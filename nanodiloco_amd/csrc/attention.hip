@@ -321,7 +321,9 @@ struct TileDma {
 };
 
 // =============================================================================== forward
-template <int HD, bool ROPE, bool DMA = false, bool PAD = false>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
+// ABL (timing ablations only, wrong results; ND_ATTN_ABL): 1 no K/V DMA + no vmcnt wait, 2 no barrier,
+// 4 no softmax (P = bf16(S)), 8 no P V MFMAs, 16 no S MFMAs (S = 0 + lane constant)
+template <int HD, bool ROPE, bool DMA = false, bool PAD = false, int ABL = 0>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
 __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int nh, int nkv, int T,
@@ -398,9 +400,9 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
     const bf16_t* Kt = Ks + (j & 1) * (BN * HD);
     const bf16_t* Vt = Vs + (j & 1) * (BN * HD);
     if constexpr (DMA) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (j + 1 < ntiles) dma_issue(j + 1);
+      if constexpr (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (!(ABL & 2)) __syncthreads();
+      if constexpr (!(ABL & 1)) if (j + 1 < ntiles) dma_issue(j + 1);
     }
     if (k0 <= q0w + 31) {  // else: whole tile above this wave's diagonal (wave-uniform)
       // K row fragments issued up front (V^T transposing reads stay next to their MFMAs: holding
@@ -415,7 +417,24 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
       for (int kt = 0; kt < 2; ++kt) {
         s[kt] = f32x16{};
 #pragma unroll
-        for (int t = 0; t < NT; ++t) s[kt] = mfma32(ka[kt][t], qf[t], s[kt]);
+        for (int t = 0; t < NT; ++t) {
+          if constexpr (ABL & 16) s[kt][t] += (float)ka[kt][t][0];
+          else s[kt] = mfma32(ka[kt][t], qf[t], s[kt]);
+        }
+      }
+      if constexpr (ABL & 4) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int sidx = 0; sidx < 2; ++sidx) {
+            const bf16x8 pf = pack_frag(s[kt], sidx);
+#pragma unroll
+            for (int o = 0; o < NO; ++o) {
+              if constexpr (ABL & 8) oacc[o][sidx] += (float)pf[o];
+              else oacc[o] = mfma32(tr_frag<HD>(Vt, kt * 32 + 16 * sidx, o * 32, g, i16), pf, oacc[o]);
+            }
+          }
+        continue;
       }
       if ((k0 + BN - 1 > q0w) || (k0 + BN > T) || (PAD && k0 < ks)) {
 #pragma unroll
@@ -461,8 +480,10 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
         for (int sidx = 0; sidx < 2; ++sidx) {
           const bf16x8 pf = pack_frag(s[kt], sidx);
 #pragma unroll
-          for (int o = 0; o < NO; ++o)
-            oacc[o] = mfma32(tr_frag<HD>(Vt, kt * 32 + 16 * sidx, o * 32, g, i16), pf, oacc[o]);
+          for (int o = 0; o < NO; ++o) {
+            if constexpr (ABL & 8) oacc[o][sidx] += (float)pf[o];
+            else oacc[o] = mfma32(tr_frag<HD>(Vt, kt * 32 + 16 * sidx, o * 32, g, i16), pf, oacc[o]);
+          }
         }
     }
     if constexpr (!DMA) {
@@ -475,6 +496,229 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
         load_tile<ROPE>(sk, Kb, ld, k0 + 2 * BN, T, cosT, sinT);
         sv.load(Vb, ld, k0 + 2 * BN, T);
       }
+    }
+  }
+  const float lt = pair_sum32(l);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qi < T) {
+    store_T<HD>(O + ((int64_t)b * T + qi) * ldo + (int64_t)head * HD, oacc, inv, h, nullptr, nullptr, 0);
+    if (h == 0) LSE[((int64_t)b * nh + head) * T + qi] = m + log2f(lt);
+  }
+}
+
+// =============================================================================== forward, pipelined
+// Software-pipelined forward (round 3; q/k already rotated, T % 64 == 0).  attn_fwd_kernel runs each
+// wave's tile as a dependency chain -- K reads -> S MFMAs -> row max -> exp / sum -> P V MFMAs -- so
+// one wave's matrix and vector work never overlap and the SIMD idles unless another wave happens to
+// be in the complementary phase (rocprof: ~25 % MFMA busy).  Here iteration j issues the S MFMAs of
+// tile j+1 in the same basic block as the exp / row sum / bf16 pack of tile j and its P V MFMAs, and
+// the row max of tile j+1 right after them: every MFMA has independent vector work beside it.
+//   * two score tiles live (sc = tile j, sn = tile j+1), deferred-max decision for tile j+1 taken
+//     at the END of iteration j (after P_j V is issued and its row sum is in l), so the rare O / l
+//     rescale multiplies exactly the terms still at the old max (guide T13 hazard);
+//   * a K/V ring of LOOK + 2 LDS slots filled by LDS-DMA LOOK tiles ahead, one barrier per tile
+//     (counted vmcnt: the younger tile's pieces stay in flight);
+//   * the causal mask touches only tile jw (the last one of the wave: 32 queries, 64-key tiles),
+//     as one compare + select per score against a per-lane limit.
+// LDS slot s: K at s * 2 * BN * HD, V at + BN * HD (swizzled soff<HD> images, as attn_fwd_kernel).
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int HD, bool PAD, int LOOK>
+__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_fwd_sp_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
+    float* __restrict__ LSE, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
+    const int* __restrict__ KS, float thr, int order) {
+  constexpr int BN = 64, NT = HD / 16, NO = HD / 32, NS = LOOK + 2;
+  constexpr int TILE = BN * HD;                               // elements of one K (or V) tile
+  constexpr int PIECES = 2 * TileDma<HD, BN>::IPW;            // DMA wave-instructions per K+V tile
+  __shared__ __attribute__((aligned(16))) bf16_t KV[NS * 2 * TILE];
+
+  const int nqb = (T + 127) / 128, bh_count = B * nh;
+  int qb, bh;
+  if (order) {  // see attn_fwd_kernel
+    const int rep = nh / nkv, grp = nqb * rep;
+    const int id = xcd_remap(blockIdx.x, nqb * bh_count);
+    const int gi = id / grp, wi = id % grp;
+    qb = nqb - 1 - wi / rep;
+    bh = (gi / nkv) * nh + (gi % nkv) * rep + wi % rep;
+  } else {
+    qb = nqb - 1 - (int)(blockIdx.x / bh_count);
+    bh = blockIdx.x % bh_count;
+  }
+  const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
+  const int ks = PAD ? KS[b] : 0;
+  const int lane = threadIdx.x & 63, h = lane >> 5, c32 = lane & 31;
+  // wave-uniform (SGPR) wave index: the per-wave tile bounds below become scalar branches
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, i16 = lane & 15;
+  const int q0w = qb * 128 + w * 32, qi = q0w + c32;
+  const float c = scale * LOG2E;
+  const bf16_t* Qb = Q + (int64_t)b * T * ld + (int64_t)head * HD;
+  const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
+  const bf16_t* Vb = V + (int64_t)b * T * ld + (int64_t)kvh * HD;
+
+  const int ntiles = min(T, qb * 128 + 128) / BN;
+  // last tile of this wave (the one holding key q0w + 31); -1: the wave is past T (T % 128 == 64)
+  const int jw = q0w < T ? (q0w + 31) / BN : -1;
+
+  // unpredicated Q loads (a row past T reads row T-1, never stored) so that every path into the
+  // tile loop has consumed them: a load still pending at the loop header would make the compiler
+  // wait vmcnt(0) -- draining the K/V DMA look-ahead -- in every iteration
+  bf16x8 qf[NT];
+  const int qr = min(qi, T - 1);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) qf[t] = load16(Qb + (int64_t)qr * ld + 16 * t + 8 * h);
+  f32x16 oacc[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) oacc[o] = f32x16{};
+  float m = -INFINITY, mref = 0.f, l = 0.f;
+
+  TileDma<HD, BN> tdma;
+  tdma.init(ld);
+  const uint32_t kv_a = lds_addr(KV);
+  auto dma_issue = [&](int j, int sl) {
+    const uint32_t a = kv_a + (uint32_t)(sl * 2 * TILE * 2);
+    tdma.issue(Kb + (int64_t)j * BN * ld, a);
+    tdma.issue(Vb + (int64_t)j * BN * ld, a + TILE * 2);
+  };
+
+  // S^T tile of keys [BN*jn, +BN) (LDS slot SL) for this wave's 32 queries; MASK: causal (+ pad) select
+  auto scores = [&](int jn, f32x16 (&s)[2], auto slot_t, auto mask_t) {
+    constexpr int SL = decltype(slot_t)::value;
+    constexpr bool MASK = decltype(mask_t)::value;
+    const bf16_t* kt_ = KV + SL * 2 * TILE;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = f32x16{};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) s[kt] = mfma32(row_frag<HD>(kt_, kt * 32 + c32, t, h), qf[t], s[kt]);
+    }
+    if constexpr (MASK) {
+      // key k0 + kt*32 + (r&3) + 8(r>>2) + 4h is visible iff <= qi (and >= ks)
+      const int lim = qi - jn * BN - 4 * h;
+      const int plim = ks - jn * BN - 4 * h;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ko = kt * 32 + (r & 3) + 8 * (r >> 2);
+          if (ko > lim || (PAD && ko < plim)) s[kt][r] = -INFINITY;
+        }
+    }
+  };
+  // raw-score row max (v_max3 tree: fmaxf on MFMA results would add canonicalising v_max per
+  // operand) -> deferred-max decision; rescales O and l
+  auto decide = [&](f32x16 (&s)[2]) {
+    float a[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = max3f(s[i >> 1][(i & 1) * 8], s[i >> 1][(i & 1) * 8 + 1], s[i >> 1][(i & 1) * 8 + 2]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x16& x = s[i >> 1];
+      const int r0 = (i & 1) * 8;
+      a[i] = max3f(a[i], x[r0 + 3], x[r0 + 4]);
+      a[i] = max3f(a[i], x[r0 + 5], x[r0 + 6]);
+      a[i] = max3f(a[i], x[r0 + 7], a[i]);
+    }
+    const float mx = pair_max32(max3f(a[0], a[1], max3f(a[2], a[3], a[3]))) * c;
+    const bool upd = mx > m + thr;
+    if (__any(upd)) {  // rare after the first tile: p <= 2^thr otherwise
+      const float mnew = upd ? mx : m;
+      const float mr = (PAD && mnew == -INFINITY) ? 0.f : mnew;
+      const float alpha = upd ? fexp2(m - mr) : 1.f;
+#pragma unroll
+      for (int o = 0; o < NO; ++o) oacc[o] *= alpha;
+      l *= alpha;
+      m = mnew;
+      mref = mr;
+    }
+  };
+  // P = exp2(c S - m) -> row sum into l, bf16 fragments -> O^T += V^T P^T (V of LDS slot SL)
+  auto softmax_pv = [&](f32x16 (&s)[2], auto slot_t) {
+    constexpr int SL = decltype(slot_t)::value;
+    const bf16_t* vt = KV + SL * 2 * TILE + TILE;
+    const float nm = -mref;
+    float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx) {
+#pragma unroll
+        for (int r = 8 * sidx; r < 8 * sidx + 8; r += 4) {
+          s[kt][r] = fexp2(fmaf(s[kt][r], c, nm));
+          s[kt][r + 1] = fexp2(fmaf(s[kt][r + 1], c, nm));
+          s[kt][r + 2] = fexp2(fmaf(s[kt][r + 2], c, nm));
+          s[kt][r + 3] = fexp2(fmaf(s[kt][r + 3], c, nm));
+          r0 += s[kt][r];
+          r1 += s[kt][r + 1];
+          r2 += s[kt][r + 2];
+          r3 += s[kt][r + 3];
+        }
+        const bf16x8 pf = pack_frag(s[kt], sidx);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) oacc[o] = mfma32(tr_frag<HD>(vt, kt * 32 + 16 * sidx, o * 32, g, i16), pf, oacc[o]);
+      }
+    l += (r0 + r1) + (r2 + r3);
+  };
+
+  // prologue: tiles 0..LOOK in flight, tile 0 landed
+  for (int p = 0; p <= LOOK && p < ntiles; ++p) dma_issue(p, p);
+  if (LOOK >= 2 && ntiles > 2) vm_wait<(LOOK >= 2 ? 2 * PIECES : 0)>();
+  else if (ntiles > 1) vm_wait<PIECES>();
+  else vm_wait<0>();
+  // the Q loads (older than the DMA) are complete here; re-define qf through an empty asm so the
+  // compiler's own wait for them lands here (a no-op) instead of inside the tile loop
+#pragma unroll
+  for (int t = 0; t < NT; ++t) asm volatile("" : "+v"(qf[t]));
+  __syncthreads();
+  f32x16 sc[2];
+  using I0 = std::integral_constant<int, 0>;
+  if (jw == 0 || PAD) scores(0, sc, I0{}, std::true_type{});
+  else scores(0, sc, I0{}, std::false_type{});
+  decide(sc);
+
+  // iteration j, tile j in LDS slot SL (compile time: the ring is unrolled NS times, so every LDS
+  // address is a per-lane base + an immediate offset)
+  auto iter = [&](int j, auto slot_t) {
+    constexpr int SL = decltype(slot_t)::value;
+    using SN = std::integral_constant<int, (SL + 1) % NS>;
+    // tile j+1 landed for every wave; every wave is done with tile j-1, whose slot takes tile j+LOOK+1
+    if (j + 1 < ntiles) {
+      if (LOOK >= 2 && j + 2 < ntiles) vm_wait<(LOOK >= 2 ? PIECES : 0)>();
+      else vm_wait<0>();
+    }
+    __syncthreads();
+    if (j + LOOK + 1 < ntiles) dma_issue(j + LOOK + 1, (SL + LOOK + 1) % NS);
+    if (j < jw) {
+      f32x16 sn[2];
+      if (j + 1 < jw && !(PAD && (j + 1) * BN < ks)) {
+        scores(j + 1, sn, SN{}, std::false_type{});
+        softmax_pv(sc, slot_t);
+      } else {
+        scores(j + 1, sn, SN{}, std::true_type{});
+        softmax_pv(sc, slot_t);
+      }
+      decide(sn);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) sc[kt] = sn[kt];
+    } else if (j == jw) {
+      softmax_pv(sc, slot_t);
+    }
+  };
+  for (int j = 0; j < ntiles; j += NS) {
+    iter(j, I0{});
+    if (j + 1 < ntiles) iter(j + 1, std::integral_constant<int, 1>{});
+    if (j + 2 < ntiles) iter(j + 2, std::integral_constant<int, 2>{});
+    if constexpr (NS > 3) {
+      if (j + 3 < ntiles) iter(j + 3, std::integral_constant<int, 3 % NS>{});
     }
   }
   const float lt = pair_sum32(l);
@@ -681,6 +925,193 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
     store_T<HD>(dQ + ((int64_t)b * T + qi) * ld + (int64_t)head * HD, dq, scale, h, ROPE_OUT ? cosT : nullptr, sinT, qi);
 }
 
+// dQ, software-pipelined (round 3; q/k already rotated, T % 64 == 0): the per-32-key-half chain of
+// attn_bwd_dq_kernel (S / dP MFMAs -> dS = P (dP - delta) on the VALU -> dQ MFMAs) is skewed by one
+// half: step u issues the S / dP MFMAs of half u+1 beside the dS vector work of half u, then the dQ
+// MFMAs of half u.  K/V ring, look-ahead, compile-time LDS slots and the diagonal-only mask as in
+// attn_fwd_sp_kernel (wave of 32 queries: only its last 32-key half u = q0w / 32 is masked).  PRE: the
+// row statistics (delta, -delta, -LSE/c for the dK/dV kernel) as in attn_bwd_dq_kernel.
+template <int HD, bool ROPE_OUT, bool PRE, bool PAD, int LOOK>
+__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_sp_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    bf16_t* __restrict__ dQ, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
+    const float* __restrict__ cosT, const float* __restrict__ sinT, const bf16_t* __restrict__ O,
+    float* __restrict__ NL, float* __restrict__ ND, const int* __restrict__ KS, int order) {
+  constexpr int BN = 64, NT = HD / 16, NO = HD / 32, NS = LOOK + 2;
+  constexpr int TILE = BN * HD;
+  constexpr int PIECES = 2 * TileDma<HD, BN>::IPW;
+  __shared__ __attribute__((aligned(16))) bf16_t KV[NS * 2 * TILE];
+
+  const int nqb = (T + 127) / 128, bh_count = B * nh;
+  int qb, bh;
+  if (order) {  // see attn_fwd_kernel
+    const int rep = nh / nkv, grp = nqb * rep;
+    const int id = xcd_remap(blockIdx.x, nqb * bh_count);
+    const int gi = id / grp, wi = id % grp;
+    qb = nqb - 1 - wi / rep;
+    bh = (gi / nkv) * nh + (gi % nkv) * rep + wi % rep;
+  } else {
+    qb = nqb - 1 - (int)(blockIdx.x / bh_count);
+    bh = blockIdx.x % bh_count;
+  }
+  const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
+  const int ks = PAD ? KS[b] : 0;
+  const int lane = threadIdx.x & 63, h = lane >> 5, c32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, i16 = lane & 15;
+  const int q0w = qb * 128 + w * 32, qi = q0w + c32;
+  const float c = scale * LOG2E;
+  const bf16_t* Qb = Q + (int64_t)b * T * ld + (int64_t)head * HD;
+  const bf16_t* dOb = dO + (int64_t)b * T * ldo + (int64_t)head * HD;
+  const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
+  const bf16_t* Vb = V + (int64_t)b * T * ld + (int64_t)kvh * HD;
+  const int ntiles = min(T, qb * 128 + 128) / BN;
+  const int uw = q0w < T ? q0w / 32 : -1;  // last (diagonal) 32-key half of this wave
+
+  TileDma<HD, BN> tdma;
+  tdma.init(ld);
+  const uint32_t kv_a = lds_addr(KV);
+  auto dma_issue = [&](int j, int sl) {
+    const uint32_t a = kv_a + (uint32_t)(sl * 2 * TILE * 2);
+    tdma.issue(Kb + (int64_t)j * BN * ld, a);
+    tdma.issue(Vb + (int64_t)j * BN * ld, a + TILE * 2);
+  };
+  for (int p = 0; p <= LOOK && p < ntiles; ++p) dma_issue(p, p);
+
+  // row operands (unpredicated: a row past T reads row T-1 and is never stored)
+  const int qr = min(qi, T - 1);
+  bf16x8 qf[NT], dof[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    qf[t] = load16(Qb + (int64_t)qr * ld + 16 * t + 8 * h);
+    dof[t] = load16(dOb + (int64_t)qr * ldo + 16 * t + 8 * h);
+  }
+  const int64_t rowstat = ((int64_t)b * nh + head) * T;
+  float lse = LSE[rowstat + qr];
+  float dlt;
+  if constexpr (PRE) {
+    float acc = 0.f;
+    const bf16_t* Orow = O + ((int64_t)b * T + qr) * ldo + (int64_t)head * HD;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const bf16x8 of = load16(Orow + 16 * t + 8 * h);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc = fmaf(bf2f((bf16_t)of[j]), bf2f((bf16_t)dof[t][j]), acc);
+    }
+    dlt = pair_sum32(acc);
+    if (qi < T && h == 0) {
+      ND[rowstat + qi] = -dlt;
+      NL[rowstat + qi] = -lse * (1.f / c);
+    }
+  } else {
+    dlt = DELTA[rowstat + qr];
+  }
+  f32x16 dq[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) dq[o] = f32x16{};
+
+  // S^T / dP^T of 32-key half KT of the tile in LDS slot SL
+  auto sdp = [&](f32x16& s, f32x16& dp, auto slot_t, auto kt_t) {
+    constexpr int SL = decltype(slot_t)::value, KT = decltype(kt_t)::value;
+    const bf16_t* kt_ = KV + SL * 2 * TILE;
+    const bf16_t* vt_ = kt_ + TILE;
+    s = f32x16{};
+    dp = f32x16{};
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      s = mfma32(row_frag<HD>(kt_, KT * 32 + c32, t, h), qf[t], s);
+      dp = mfma32(row_frag<HD>(vt_, KT * 32 + c32, t, h), dof[t], dp);
+    }
+  };
+  // dS = P (dP - delta) of half u, then dQ^T += K^T dS^T (K of slot SL, half KT)
+  auto ds_dq = [&](f32x16& s, f32x16& dp, int u, auto slot_t, auto kt_t, auto mask_t) {
+    constexpr int SL = decltype(slot_t)::value, KT = decltype(kt_t)::value;
+    constexpr bool MASK = decltype(mask_t)::value;
+    if constexpr (MASK) {  // select after the exp: a pad query row has lse = -inf
+      const int lim = qi - u * 32 - 4 * h, plim = ks - u * 32 - 4 * h;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ko = (r & 3) + 8 * (r >> 2);
+        const float p = (ko > lim || (PAD && ko < plim)) ? 0.f : fexp2(fmaf(s[r], c, -lse));
+        dp[r] = p * (dp[r] - dlt);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dp[r] = fexp2(fmaf(s[r], c, -lse)) * (dp[r] - dlt);
+    }
+    const bf16_t* kt_ = KV + SL * 2 * TILE;
+#pragma unroll
+    for (int sidx = 0; sidx < 2; ++sidx) {
+      const bf16x8 dsf = pack_frag(dp, sidx);
+#pragma unroll
+      for (int o = 0; o < NO; ++o) dq[o] = mfma32(tr_frag<HD>(kt_, KT * 32 + 16 * sidx, o * 32, g, i16), dsf, dq[o]);
+    }
+  };
+
+  if (LOOK >= 2 && ntiles > 2) vm_wait<(LOOK >= 2 ? 2 * PIECES : 0)>();
+  else if (ntiles > 1) vm_wait<PIECES>();
+  else vm_wait<0>();
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    asm volatile("" : "+v"(qf[t]));
+    asm volatile("" : "+v"(dof[t]));
+  }
+  asm volatile("" : "+v"(lse), "+v"(dlt));
+  __syncthreads();
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using TT = std::true_type;
+  using FF = std::false_type;
+  f32x16 s, dp;
+  sdp(s, dp, I0{}, I0{});
+
+  auto iter = [&](int j, auto slot_t) {
+    constexpr int SL = decltype(slot_t)::value;
+    using SN = std::integral_constant<int, (SL + 1) % NS>;
+    if (j + 1 < ntiles) {
+      if (LOOK >= 2 && j + 2 < ntiles) vm_wait<(LOOK >= 2 ? PIECES : 0)>();
+      else vm_wait<0>();
+    }
+    __syncthreads();
+    if (j + LOOK + 1 < ntiles) dma_issue(j + LOOK + 1, (SL + LOOK + 1) % NS);
+    // half 2j (next: half 2j+1, same tile)
+    const int u0 = 2 * j;
+    if (u0 < uw) {
+      f32x16 s2, dp2;
+      sdp(s2, dp2, slot_t, I1{});
+      if (PAD && u0 * 32 < ks) ds_dq(s, dp, u0, slot_t, I0{}, TT{});
+      else ds_dq(s, dp, u0, slot_t, I0{}, FF{});
+      s = s2;
+      dp = dp2;
+    } else if (u0 == uw) {
+      ds_dq(s, dp, u0, slot_t, I0{}, TT{});
+    }
+    // half 2j+1 (next: half 2j+2 = first half of tile j+1, landed at this iteration's barrier)
+    const int u1 = 2 * j + 1;
+    if (u1 < uw) {
+      f32x16 s2, dp2;
+      sdp(s2, dp2, SN{}, I0{});
+      if (PAD && u1 * 32 < ks) ds_dq(s, dp, u1, slot_t, I1{}, TT{});
+      else ds_dq(s, dp, u1, slot_t, I1{}, FF{});
+      s = s2;
+      dp = dp2;
+    } else if (u1 == uw) {
+      ds_dq(s, dp, u1, slot_t, I1{}, TT{});
+    }
+  };
+  for (int j = 0; j < ntiles; j += NS) {
+    iter(j, I0{});
+    if (j + 1 < ntiles) iter(j + 1, I1{});
+    if (j + 2 < ntiles) iter(j + 2, std::integral_constant<int, 2>{});
+    if constexpr (NS > 3) {
+      if (j + 3 < ntiles) iter(j + 3, std::integral_constant<int, 3 % NS>{});
+    }
+  }
+  if (qi < T)
+    store_T<HD>(dQ + ((int64_t)b * T + qi) * ld + (int64_t)head * HD, dq, scale, h, ROPE_OUT ? cosT : nullptr, sinT, qi);
+}
+
 // dK, dV: per 128 keys of one (b, kv head); loops over the GQA group's query heads and 64-query
 // tiles from the diagonal to T.
 template <int HD, bool ROPE, bool ROPE_OUT, bool PAD = false>
@@ -862,12 +1293,40 @@ static int fwd_launch(const void* q, const void* k, const void* v, void* o, floa
   // deferred-max threshold (log2 units; ND_ATTN_THR for A/B, 0 = move the max on every increase)
   const char* te = getenv("ND_ATTN_THR");
   const float thr = te ? (float)atof(te) : 8.f;
+  // ND_ATTN_FWD: 'r' register-staged, 's' the pipelined kernel (ND_ATTN_LOOK = DMA look-ahead in
+  // tiles, 1 or 2; measured 0.89x, not the default), else the LDS-DMA kernel
+  const char* fe = getenv("ND_ATTN_FWD");
+  const char fv = fe ? fe[0] : 'd';
+  if constexpr (HD <= 64) {
+    if (!cosT && T % 64 == 0 && fv == 's') {
+      const char* le = getenv("ND_ATTN_LOOK");
+      if (le && le[0] == '2')
+        hipLaunchKernelGGL((attn_fwd_sp_kernel<HD, PAD, 2>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k,
+                           (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, ks, thr, attn_order());
+      else
+        hipLaunchKernelGGL((attn_fwd_sp_kernel<HD, PAD, 1>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k,
+                           (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, ks, thr, attn_order());
+      ND_LAUNCH_CHECK();
+    }
+  }
   if (cosT)
     hipLaunchKernelGGL((attn_fwd_kernel<HD, true, false, PAD>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr, attn_order());
-  else if (T % 64 == 0 && !(getenv("ND_ATTN_FWD") && getenv("ND_ATTN_FWD")[0] == 'r'))
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, false, true, PAD>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr, attn_order());
+  else if (T % 64 == 0 && fv != 'r') {
+    const char* ae = getenv("ND_ATTN_ABL");
+    const int abl = ae ? atoi(ae) : 0;
+#define ND_ABL(A)                                                                                                  \
+  case A:                                                                                                          \
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, false, true, PAD, A>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, \
+                       (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr,      \
+                       attn_order());                                                                              \
+    break;
+    switch (PAD ? 0 : abl) {
+      ND_ABL(1) ND_ABL(2) ND_ABL(3) ND_ABL(4) ND_ABL(7) ND_ABL(8) ND_ABL(12) ND_ABL(16) ND_ABL(20) ND_ABL(24) ND_ABL(28)
+      default: ND_ABL(0)
+    }
+#undef ND_ABL
+  }
   else
     hipLaunchKernelGGL((attn_fwd_kernel<HD, false, false, PAD>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr, attn_order());
@@ -1176,9 +1635,30 @@ static int bwd_fused_launch(const void* q, const void* k, const void* v, const v
   const int nb = (T + 127) / 128;
   const int64_t n = (int64_t)B * nh * T;
   float *nl = ws, *nd = ws + n;
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, ROPE_OUT, true, true, PAD>), dim3(nb * B * nh), dim3(256), 0, s,
-                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
-                     (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks, attn_order());
+  // ND_ATTN_DQ: 's' = the pipelined dQ kernel (HD <= 64; ND_ATTN_LOOK as the forward; measured 0.97x,
+  // not the default), else attn_bwd_dq_kernel
+  const char* qe = getenv("ND_ATTN_DQ");
+  const char* le = getenv("ND_ATTN_LOOK");
+  bool done = false;
+  if constexpr (HD <= 64) {
+    if (qe && qe[0] == 's') {
+      if (le && le[0] == '2')
+        hipLaunchKernelGGL((attn_bwd_dq_sp_kernel<HD, ROPE_OUT, true, PAD, 2>), dim3(nb * B * nh), dim3(256), 0, s,
+                           (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
+                           (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks,
+                           attn_order());
+      else
+        hipLaunchKernelGGL((attn_bwd_dq_sp_kernel<HD, ROPE_OUT, true, PAD, 1>), dim3(nb * B * nh), dim3(256), 0, s,
+                           (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
+                           (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks,
+                           attn_order());
+      done = true;
+    }
+  }
+  if (!done)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, ROPE_OUT, true, true, PAD>), dim3(nb * B * nh), dim3(256), 0, s,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
+                       (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks, attn_order());
   if (T % 128 == 0)
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,

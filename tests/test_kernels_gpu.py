@@ -514,3 +514,87 @@ def _store_view(store, flat, name):
     v = store.grad_view(name)
     off = (v.data_ptr() - store.grad.data_ptr()) // v.element_size()
     return flat[off:off + v.numel()]
+
+
+@pytest.mark.parametrize("B,T,nh,nkv,hd,pads", [
+    (2, 64, 2, 2, 64, None), (2, 192, 4, 2, 64, None), (1, 1024, 4, 4, 64, None), (3, 512, 8, 2, 64, None),
+    (2, 320, 4, 4, 32, None), (2, 256, 4, 4, 64, (0, 100)), (2, 1024, 16, 16, 64, (0, 700)),
+])
+@pytest.mark.parametrize("variant", ["s1", "s2", "d", "r"])
+def test_attention_fwd_variants(B, T, nh, nkv, hd, pads, variant, monkeypatch):
+    """Forward kernels on pre-rotated q|k (the fused-RoPE path): the software-pipelined kernel with a
+    1- and 2-tile K/V look-ahead (default 's1') and the round-2 LDS-DMA kernel ('d') against fp32
+    torch, output and log-sum-exp; T % 128 == 64 leaves idle waves in the last query block."""
+    from nanodiloco_amd.ops import _ext
+    from nanodiloco_amd.ops.attention import key_start
+    monkeypatch.setenv("ND_ATTN_FWD", variant[0])
+    monkeypatch.setenv("ND_ATTN_LOOK", variant[1:] or "1")
+    ld = (nh + 2 * nkv) * hd
+    qkv = torch.randn(B * T, ld, device=DEV).bfloat16()
+    qkv[T // 2, nh * hd:(nh + 1) * hd] *= 20  # a late key with a large score: deferred-max rescale path
+    k, v = qkv[:, nh * hd:], qkv[:, (nh + nkv) * hd:]
+    ks = None
+    if pads is not None:
+        mask = torch.ones(B, T, dtype=torch.long, device=DEV)
+        for b, p in enumerate(pads):
+            mask[b, :p] = 0
+        ks = key_start(mask)
+    o = torch.empty(B * T, nh * hd, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, nh, T, device=DEV)
+    L = _ext.lib()
+    _ext.check(L.nd_attn_fwd_ks(qkv.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(), B, nh, nkv, T,
+                                hd, ld, nh * hd, 0, 0, hd ** -0.5, ks.data_ptr() if ks is not None else 0,
+                                _ext.stream_ptr(qkv.device)), "fwd")
+    q4, k4, v4 = ref.split_qkv(qkv.float(), B, T, nh, nkv, hd)
+    rep = nh // nkv
+    k4, v4 = k4.repeat_interleave(rep, 1), v4.repeat_interleave(rep, 1)
+    s = (q4 @ k4.transpose(-1, -2)) * hd ** -0.5
+    i = torch.arange(T, device=DEV)
+    allowed = (i[None, :] <= i[:, None])[None, None].expand(B, 1, T, T).clone()
+    if ks is not None:
+        allowed &= (i[None, None, None, :] >= ks[:, None, None, None])
+    s = s.masked_fill(~allowed, float("-inf"))
+    lse_ref = torch.logsumexp(s, -1)  # natural log; the kernel stores log2 units
+    p = torch.softmax(s, -1).nan_to_num(0.0)
+    oref = (p @ v4).transpose(1, 2).reshape(B * T, nh * hd)
+    assert torch.isfinite(o.float()).all()
+    assert rel(o, oref) < 1e-2, rel(o, oref)
+    valid = torch.isfinite(lse_ref)
+    assert (lse[valid] / 1.4426950408889634 - lse_ref[valid]).abs().max().item() < 2e-2
+    if ks is not None:
+        pad_rows = ~allowed[:, 0].any(-1).reshape(-1)
+        assert (o[pad_rows] == 0).all()
+
+
+@pytest.mark.parametrize("B,T,nh,nkv,hd,pads", [
+    (2, 64, 2, 2, 64, None), (2, 192, 4, 2, 64, None), (1, 1024, 4, 4, 64, None), (2, 320, 4, 4, 32, None),
+    (2, 256, 4, 4, 64, (0, 100)), (2, 1024, 8, 2, 64, (0, 700)),
+])
+@pytest.mark.parametrize("variant", ["s1", "s2", "o"])
+def test_attention_bwd_dq_variants(B, T, nh, nkv, hd, pads, variant, monkeypatch):
+    """Fused backward (dQ kernel with the row statistics, then dK/dV) with the software-pipelined dQ
+    kernel (1- / 2-tile look-ahead) and the round-2 one ('o'): all three gradients against fp32."""
+    from nanodiloco_amd.ops.attention import key_start, rope_cache
+    monkeypatch.setenv("ND_ATTN_DQ", variant[0])
+    monkeypatch.setenv("ND_ATTN_LOOK", variant[1:] or "1")
+    ld = (nh + 2 * nkv) * hd
+    ks = None
+    if pads is not None:
+        mask = torch.ones(B, T, dtype=torch.long, device=DEV)
+        for b, p in enumerate(pads):
+            mask[b, :p] = 0
+        ks = key_start(mask)
+    qkv = torch.randn(B * T, ld, device=DEV).bfloat16()
+    cos, sin = rope_cache(T, hd, 10000.0, None, DEV)
+    x = qkv.clone().requires_grad_(True)
+    o = ops.attention(x, cos, sin, B, T, nh, nkv, hd, kstart=ks)
+    xr = qkv.float().requires_grad_(True)
+    orf = ref.attention_block(xr, cos, sin, B, T, nh, nkv, hd, kstart=ks)
+    do = torch.randn_like(orf)
+    o.backward(do.bfloat16())
+    orf.backward(do.bfloat16().float())
+    g, gr = x.grad.float(), xr.grad
+    assert torch.isfinite(g).all()
+    nq, nk = nh * hd, nkv * hd
+    for name, sl in (("dq", slice(0, nq)), ("dk", slice(nq, nq + nk)), ("dv", slice(nq + nk, None))):
+        assert rel(g[:, sl], gr[:, sl]) < 3e-2, (name, rel(g[:, sl], gr[:, sl]))
