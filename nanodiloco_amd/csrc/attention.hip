@@ -298,9 +298,9 @@ __device__ __forceinline__ uint32_t lds_addr(const T_* p) {
 
 // LDS-DMA of one ROWS x HD bf16 tile (row stride ld) into a soff<HD>-swizzled LDS tile by the 4 waves
 // of a workgroup: 1-KiB wave-instructions of 64/CPR rows, per-lane source offsets fixed per kernel.
-template <int HD, int ROWS>
+template <int HD, int ROWS, int NW = 4>  // NW waves share the tile
 struct TileDma {
-  static constexpr int CPR = HD / 8, RPI = 64 / CPR, IPW = (ROWS / RPI) / 4;
+  static constexpr int CPR = HD / 8, RPI = 64 / CPR, IPW = (ROWS / RPI) / NW;
   uint32_t voff[IPW];
   int wu;
   __device__ __forceinline__ void init(int64_t ld) {
@@ -308,7 +308,7 @@ struct TileDma {
     wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
-      const int row = (wu + 4 * i) * RPI + lane / CPR, p = lane % CPR;
+      const int row = (wu + NW * i) * RPI + lane / CPR, p = lane % CPR;
       const int lch = (soff<HD>(row, p * 8) - row * HD) / 8;  // XOR swizzle: physical p holds logical lch
       voff[i] = (uint32_t)(((int64_t)row * ld + lch * 8) * 2);
     }
@@ -316,15 +316,23 @@ struct TileDma {
   // rows row0.. of `base` (already offset to the tile's first row) -> LDS tile at byte address `lds`
   __device__ __forceinline__ void issue(const bf16_t* base, uint32_t lds) const {
 #pragma unroll
-    for (int i = 0; i < IPW; ++i) adma_b128(base, voff[i], lds + (uint32_t)((wu + 4 * i) * 1024));
+    for (int i = 0; i < IPW; ++i) adma_b128(base, voff[i], lds + (uint32_t)((wu + NW * i) * 1024));
   }
 };
 
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // =============================================================================== forward
 // ABL (timing ablations only, wrong results; ND_ATTN_ABL): 1 no K/V DMA + no vmcnt wait, 2 no barrier,
-// 4 no softmax (P = bf16(S)), 8 no P V MFMAs, 16 no S MFMAs (S = 0 + lane constant)
-template <int HD, bool ROPE, bool DMA = false, bool PAD = false, int ABL = 0>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
-__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+// 4 no softmax (P = bf16(S)), 8 no P V MFMAs, 16 no S MFMAs (S = 0 + lane constant).  Bit 32 is a
+// correct variant (cheaper mask, max tree, split row sum: needs T % 64 == 0).
+// NW: waves per workgroup (4 or 8; 8 = 256-query blocks, every K/V tile DMA'd once per 256 queries: DMA only)
+template <int HD, bool ROPE, bool DMA = false, bool PAD = false, int ABL = 0, int NW = 4>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
+__global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int nh, int nkv, int T,
                                                           int64_t ld, int64_t ldo, float scale,
@@ -334,7 +342,9 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * BN * HD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * BN * HD];
 
-  const int nqb = (T + 127) / 128, bh_count = B * nh;
+  constexpr int QB = 32 * NW;  // queries per workgroup
+  static_assert(NW == 4 || (NW == 8 && DMA), "8-wave blocks: LDS-DMA staging only");
+  const int nqb = (T + QB - 1) / QB, bh_count = B * nh;
   // order 0: q-block major (longest causal rows of every head first); 1: the q-blocks of one
   // (batch, head) run together on one XCD, so its K/V tiles are fetched from HBM once and re-read from L2
   int qb, bh;
@@ -354,7 +364,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
   const int ks = PAD ? KS[b] : 0;  // PAD (left-padded batch): keys < ks are masked for every query
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15;
-  const int q0w = qb * 128 + w * 32, qi = q0w + c32;
+  const int q0w = qb * QB + w * 32, qi = q0w + c32;
   const float c = scale * LOG2E;
   const bf16_t* Qb = Q + (int64_t)b * T * ld + (int64_t)head * HD;
   const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
@@ -369,10 +379,10 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
   for (int o = 0; o < NO; ++o) oacc[o] = f32x16{};
   float m = -INFINITY, l = 0.f;
 
-  const int ntiles = (min(T, qb * 128 + 128) + BN - 1) / BN;
+  const int ntiles = (min(T, qb * QB + QB) + BN - 1) / BN;
   typename std::conditional<ROPE, StageRope<BN, HD>, Stage<BN, HD>>::type sk;
   Stage<BN, HD> sv;
-  TileDma<HD, BN> tdma;
+  TileDma<HD, BN, NW> tdma;
   const uint32_t ks_a = lds_addr(Ks), vs_a = lds_addr(Vs);
   auto dma_issue = [&](int j) {
     const uint32_t off = (uint32_t)((j & 1) * BN * HD * 2);
@@ -436,21 +446,48 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
           }
         continue;
       }
-      if ((k0 + BN - 1 > q0w) || (k0 + BN > T) || (PAD && k0 < ks)) {
+      float mx;
+      if constexpr (ABL & 32) {
+        // variant 32: one compare + select per score against a per-lane limit (T % 64 == 0 here: no
+        // key >= T), row max as four independent v_max3 chains
+        if ((k0 + BN - 1 > q0w) || (PAD && k0 < ks)) {
+          const int lim = qi - k0 - 4 * h, plim = ks - k0 - 4 * h;
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int ko = kt * 32 + (r & 3) + 8 * (r >> 2);
+              if (ko > lim || (PAD && ko < plim)) s[kt][r] = -INFINITY;
+            }
+        }
+        float a4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x16& x = s[i >> 1];
+          const int r0 = (i & 1) * 8;
+          a4[i] = max3f(x[r0], x[r0 + 1], x[r0 + 2]);
+          a4[i] = max3f(a4[i], x[r0 + 3], x[r0 + 4]);
+          a4[i] = max3f(a4[i], x[r0 + 5], x[r0 + 6]);
+          a4[i] = max3f(a4[i], x[r0 + 7], a4[i]);
+        }
+        mx = pair_max32(max3f(a4[0], a4[1], max3f(a4[2], a4[3], a4[3]))) * c;
+      } else {
+        if ((k0 + BN - 1 > q0w) || (k0 + BN > T) || (PAD && k0 < ks)) {
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              if (key > qi || key >= T || (PAD && key < ks)) s[kt][r] = -INFINITY;
+            }
+        }
+        mx = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (key > qi || key >= T || (PAD && key < ks)) s[kt][r] = -INFINITY;
-          }
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
+        mx = pair_max32(mx) * c;  // raw-score max -> log2 domain (c > 0)
       }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
-      mx = pair_max32(mx) * c;  // raw-score max -> log2 domain (c > 0)
       // deferred max (guide T13): the running max moves only when the tile's max exceeds it by more
       // than thr (log2 units), so p <= 2^thr and the O rescale below is skipped on almost every tile.
       // Both lanes of a query pair see the same m / mx, so l and O get one consistent factor.
@@ -460,6 +497,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
       const float mref = (PAD && mnew == -INFINITY) ? 0.f : mnew;
       const float alpha = upd ? fexp2(m - mref) : 1.f;
       m = mnew;
+      float rs4[4] = {0.f, 0.f, 0.f, 0.f};  // variant 32: four independent partial sums
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -467,8 +505,10 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
         for (int r = 0; r < 16; ++r) {
           const float p = fexp2(fmaf(s[kt][r], c, -mref));
           s[kt][r] = p;
-          rs += p;
+          if constexpr (ABL & 32) rs4[r & 3] += p;
+          else rs += p;
         }
+      if constexpr (ABL & 32) rs = (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);
       l = l * alpha + rs;
       if (__any(alpha != 1.f)) {
 #pragma unroll
@@ -496,229 +536,6 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(cons
         load_tile<ROPE>(sk, Kb, ld, k0 + 2 * BN, T, cosT, sinT);
         sv.load(Vb, ld, k0 + 2 * BN, T);
       }
-    }
-  }
-  const float lt = pair_sum32(l);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (qi < T) {
-    store_T<HD>(O + ((int64_t)b * T + qi) * ldo + (int64_t)head * HD, oacc, inv, h, nullptr, nullptr, 0);
-    if (h == 0) LSE[((int64_t)b * nh + head) * T + qi] = m + log2f(lt);
-  }
-}
-
-// =============================================================================== forward, pipelined
-// Software-pipelined forward (round 3; q/k already rotated, T % 64 == 0).  attn_fwd_kernel runs each
-// wave's tile as a dependency chain -- K reads -> S MFMAs -> row max -> exp / sum -> P V MFMAs -- so
-// one wave's matrix and vector work never overlap and the SIMD idles unless another wave happens to
-// be in the complementary phase (rocprof: ~25 % MFMA busy).  Here iteration j issues the S MFMAs of
-// tile j+1 in the same basic block as the exp / row sum / bf16 pack of tile j and its P V MFMAs, and
-// the row max of tile j+1 right after them: every MFMA has independent vector work beside it.
-//   * two score tiles live (sc = tile j, sn = tile j+1), deferred-max decision for tile j+1 taken
-//     at the END of iteration j (after P_j V is issued and its row sum is in l), so the rare O / l
-//     rescale multiplies exactly the terms still at the old max (guide T13 hazard);
-//   * a K/V ring of LOOK + 2 LDS slots filled by LDS-DMA LOOK tiles ahead, one barrier per tile
-//     (counted vmcnt: the younger tile's pieces stay in flight);
-//   * the causal mask touches only tile jw (the last one of the wave: 32 queries, 64-key tiles),
-//     as one compare + select per score against a per-lane limit.
-// LDS slot s: K at s * 2 * BN * HD, V at + BN * HD (swizzled soff<HD> images, as attn_fwd_kernel).
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int HD, bool PAD, int LOOK>
-__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_fwd_sp_kernel(
-    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
-    float* __restrict__ LSE, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
-    const int* __restrict__ KS, float thr, int order) {
-  constexpr int BN = 64, NT = HD / 16, NO = HD / 32, NS = LOOK + 2;
-  constexpr int TILE = BN * HD;                               // elements of one K (or V) tile
-  constexpr int PIECES = 2 * TileDma<HD, BN>::IPW;            // DMA wave-instructions per K+V tile
-  __shared__ __attribute__((aligned(16))) bf16_t KV[NS * 2 * TILE];
-
-  const int nqb = (T + 127) / 128, bh_count = B * nh;
-  int qb, bh;
-  if (order) {  // see attn_fwd_kernel
-    const int rep = nh / nkv, grp = nqb * rep;
-    const int id = xcd_remap(blockIdx.x, nqb * bh_count);
-    const int gi = id / grp, wi = id % grp;
-    qb = nqb - 1 - wi / rep;
-    bh = (gi / nkv) * nh + (gi % nkv) * rep + wi % rep;
-  } else {
-    qb = nqb - 1 - (int)(blockIdx.x / bh_count);
-    bh = blockIdx.x % bh_count;
-  }
-  const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
-  const int ks = PAD ? KS[b] : 0;
-  const int lane = threadIdx.x & 63, h = lane >> 5, c32 = lane & 31;
-  // wave-uniform (SGPR) wave index: the per-wave tile bounds below become scalar branches
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4, i16 = lane & 15;
-  const int q0w = qb * 128 + w * 32, qi = q0w + c32;
-  const float c = scale * LOG2E;
-  const bf16_t* Qb = Q + (int64_t)b * T * ld + (int64_t)head * HD;
-  const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
-  const bf16_t* Vb = V + (int64_t)b * T * ld + (int64_t)kvh * HD;
-
-  const int ntiles = min(T, qb * 128 + 128) / BN;
-  // last tile of this wave (the one holding key q0w + 31); -1: the wave is past T (T % 128 == 64)
-  const int jw = q0w < T ? (q0w + 31) / BN : -1;
-
-  // unpredicated Q loads (a row past T reads row T-1, never stored) so that every path into the
-  // tile loop has consumed them: a load still pending at the loop header would make the compiler
-  // wait vmcnt(0) -- draining the K/V DMA look-ahead -- in every iteration
-  bf16x8 qf[NT];
-  const int qr = min(qi, T - 1);
-#pragma unroll
-  for (int t = 0; t < NT; ++t) qf[t] = load16(Qb + (int64_t)qr * ld + 16 * t + 8 * h);
-  f32x16 oacc[NO];
-#pragma unroll
-  for (int o = 0; o < NO; ++o) oacc[o] = f32x16{};
-  float m = -INFINITY, mref = 0.f, l = 0.f;
-
-  TileDma<HD, BN> tdma;
-  tdma.init(ld);
-  const uint32_t kv_a = lds_addr(KV);
-  auto dma_issue = [&](int j, int sl) {
-    const uint32_t a = kv_a + (uint32_t)(sl * 2 * TILE * 2);
-    tdma.issue(Kb + (int64_t)j * BN * ld, a);
-    tdma.issue(Vb + (int64_t)j * BN * ld, a + TILE * 2);
-  };
-
-  // S^T tile of keys [BN*jn, +BN) (LDS slot SL) for this wave's 32 queries; MASK: causal (+ pad) select
-  auto scores = [&](int jn, f32x16 (&s)[2], auto slot_t, auto mask_t) {
-    constexpr int SL = decltype(slot_t)::value;
-    constexpr bool MASK = decltype(mask_t)::value;
-    const bf16_t* kt_ = KV + SL * 2 * TILE;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      s[kt] = f32x16{};
-#pragma unroll
-      for (int t = 0; t < NT; ++t) s[kt] = mfma32(row_frag<HD>(kt_, kt * 32 + c32, t, h), qf[t], s[kt]);
-    }
-    if constexpr (MASK) {
-      // key k0 + kt*32 + (r&3) + 8(r>>2) + 4h is visible iff <= qi (and >= ks)
-      const int lim = qi - jn * BN - 4 * h;
-      const int plim = ks - jn * BN - 4 * h;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ko = kt * 32 + (r & 3) + 8 * (r >> 2);
-          if (ko > lim || (PAD && ko < plim)) s[kt][r] = -INFINITY;
-        }
-    }
-  };
-  // raw-score row max (v_max3 tree: fmaxf on MFMA results would add canonicalising v_max per
-  // operand) -> deferred-max decision; rescales O and l
-  auto decide = [&](f32x16 (&s)[2]) {
-    float a[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = max3f(s[i >> 1][(i & 1) * 8], s[i >> 1][(i & 1) * 8 + 1], s[i >> 1][(i & 1) * 8 + 2]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f32x16& x = s[i >> 1];
-      const int r0 = (i & 1) * 8;
-      a[i] = max3f(a[i], x[r0 + 3], x[r0 + 4]);
-      a[i] = max3f(a[i], x[r0 + 5], x[r0 + 6]);
-      a[i] = max3f(a[i], x[r0 + 7], a[i]);
-    }
-    const float mx = pair_max32(max3f(a[0], a[1], max3f(a[2], a[3], a[3]))) * c;
-    const bool upd = mx > m + thr;
-    if (__any(upd)) {  // rare after the first tile: p <= 2^thr otherwise
-      const float mnew = upd ? mx : m;
-      const float mr = (PAD && mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = upd ? fexp2(m - mr) : 1.f;
-#pragma unroll
-      for (int o = 0; o < NO; ++o) oacc[o] *= alpha;
-      l *= alpha;
-      m = mnew;
-      mref = mr;
-    }
-  };
-  // P = exp2(c S - m) -> row sum into l, bf16 fragments -> O^T += V^T P^T (V of LDS slot SL)
-  auto softmax_pv = [&](f32x16 (&s)[2], auto slot_t) {
-    constexpr int SL = decltype(slot_t)::value;
-    const bf16_t* vt = KV + SL * 2 * TILE + TILE;
-    const float nm = -mref;
-    float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int sidx = 0; sidx < 2; ++sidx) {
-#pragma unroll
-        for (int r = 8 * sidx; r < 8 * sidx + 8; r += 4) {
-          s[kt][r] = fexp2(fmaf(s[kt][r], c, nm));
-          s[kt][r + 1] = fexp2(fmaf(s[kt][r + 1], c, nm));
-          s[kt][r + 2] = fexp2(fmaf(s[kt][r + 2], c, nm));
-          s[kt][r + 3] = fexp2(fmaf(s[kt][r + 3], c, nm));
-          r0 += s[kt][r];
-          r1 += s[kt][r + 1];
-          r2 += s[kt][r + 2];
-          r3 += s[kt][r + 3];
-        }
-        const bf16x8 pf = pack_frag(s[kt], sidx);
-#pragma unroll
-        for (int o = 0; o < NO; ++o) oacc[o] = mfma32(tr_frag<HD>(vt, kt * 32 + 16 * sidx, o * 32, g, i16), pf, oacc[o]);
-      }
-    l += (r0 + r1) + (r2 + r3);
-  };
-
-  // prologue: tiles 0..LOOK in flight, tile 0 landed
-  for (int p = 0; p <= LOOK && p < ntiles; ++p) dma_issue(p, p);
-  if (LOOK >= 2 && ntiles > 2) vm_wait<(LOOK >= 2 ? 2 * PIECES : 0)>();
-  else if (ntiles > 1) vm_wait<PIECES>();
-  else vm_wait<0>();
-  // the Q loads (older than the DMA) are complete here; re-define qf through an empty asm so the
-  // compiler's own wait for them lands here (a no-op) instead of inside the tile loop
-#pragma unroll
-  for (int t = 0; t < NT; ++t) asm volatile("" : "+v"(qf[t]));
-  __syncthreads();
-  f32x16 sc[2];
-  using I0 = std::integral_constant<int, 0>;
-  if (jw == 0 || PAD) scores(0, sc, I0{}, std::true_type{});
-  else scores(0, sc, I0{}, std::false_type{});
-  decide(sc);
-
-  // iteration j, tile j in LDS slot SL (compile time: the ring is unrolled NS times, so every LDS
-  // address is a per-lane base + an immediate offset)
-  auto iter = [&](int j, auto slot_t) {
-    constexpr int SL = decltype(slot_t)::value;
-    using SN = std::integral_constant<int, (SL + 1) % NS>;
-    // tile j+1 landed for every wave; every wave is done with tile j-1, whose slot takes tile j+LOOK+1
-    if (j + 1 < ntiles) {
-      if (LOOK >= 2 && j + 2 < ntiles) vm_wait<(LOOK >= 2 ? PIECES : 0)>();
-      else vm_wait<0>();
-    }
-    __syncthreads();
-    if (j + LOOK + 1 < ntiles) dma_issue(j + LOOK + 1, (SL + LOOK + 1) % NS);
-    if (j < jw) {
-      f32x16 sn[2];
-      if (j + 1 < jw && !(PAD && (j + 1) * BN < ks)) {
-        scores(j + 1, sn, SN{}, std::false_type{});
-        softmax_pv(sc, slot_t);
-      } else {
-        scores(j + 1, sn, SN{}, std::true_type{});
-        softmax_pv(sc, slot_t);
-      }
-      decide(sn);
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) sc[kt] = sn[kt];
-    } else if (j == jw) {
-      softmax_pv(sc, slot_t);
-    }
-  };
-  for (int j = 0; j < ntiles; j += NS) {
-    iter(j, I0{});
-    if (j + 1 < ntiles) iter(j + 1, std::integral_constant<int, 1>{});
-    if (j + 2 < ntiles) iter(j + 2, std::integral_constant<int, 2>{});
-    if constexpr (NS > 3) {
-      if (j + 3 < ntiles) iter(j + 3, std::integral_constant<int, 3 % NS>{});
     }
   }
   const float lt = pair_sum32(l);
@@ -764,8 +581,9 @@ __global__ void __launch_bounds__(256) attn_bwd_pre_kernel(const bf16_t* __restr
 // attn_neg_stats_kernel: each lane already holds half of its query's dO row, so it loads the same
 // half of O, dots, and one lane^32 exchange gives delta = rowsum(dO * O); the kernel then writes
 // -delta and -LSE/c (the seeds of the dK/dV kernel, which therefore runs after this one).
-template <int HD, bool ROPE, bool ROPE_OUT, bool DMA = false, bool PRE = false, bool PAD = false>  // DMA: LDS-DMA K/V staging
-__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+// NW: waves per workgroup (8 = 256-query blocks, LDS-DMA only; see attn_fwd_kernel)
+template <int HD, bool ROPE, bool ROPE_OUT, bool DMA = false, bool PRE = false, bool PAD = false, int NW = 4>  // DMA: LDS-DMA K/V staging
+__global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                              const bf16_t* __restrict__ V, const bf16_t* __restrict__ dO,
                                                              const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                              bf16_t* __restrict__ dQ, int B, int nh, int nkv, int T,
@@ -779,7 +597,9 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * BN * HD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * BN * HD];
 
-  const int nqb = (T + 127) / 128, bh_count = B * nh;
+  constexpr int QB = 32 * NW;
+  static_assert(NW == 4 || (NW == 8 && DMA), "8-wave blocks: LDS-DMA staging only");
+  const int nqb = (T + QB - 1) / QB, bh_count = B * nh;
   int qb, bh;
   if (order) {  // see attn_fwd_kernel
     const int rep = nh / nkv, grp = nqb * rep;
@@ -795,7 +615,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
   const int ks = PAD ? KS[b] : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15;
-  const int q0w = qb * 128 + w * 32, qi = q0w + c32;
+  const int q0w = qb * QB + w * 32, qi = q0w + c32;
   const float c = scale * LOG2E;
   const bf16_t* Qb = Q + (int64_t)b * T * ld + (int64_t)head * HD;
   const bf16_t* dOb = dO + (int64_t)b * T * ldo + (int64_t)head * HD;
@@ -835,10 +655,10 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
 #pragma unroll
   for (int o = 0; o < NO; ++o) dq[o] = f32x16{};
 
-  const int ntiles = (min(T, qb * 128 + 128) + BN - 1) / BN;
+  const int ntiles = (min(T, qb * QB + QB) + BN - 1) / BN;
   typename std::conditional<ROPE, StageRope<BN, HD>, Stage<BN, HD>>::type sk;
   Stage<BN, HD> sv;
-  TileDma<HD, BN> tdma;
+  TileDma<HD, BN, NW> tdma;
   const uint32_t ks_a = lds_addr(Ks), vs_a = lds_addr(Vs);
   auto dma_issue = [&](int j) {
     const uint32_t off = (uint32_t)((j & 1) * BN * HD * 2);
@@ -919,193 +739,6 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(c
         load_tile<ROPE>(sk, Kb, ld, k0 + 2 * BN, T, cosT, sinT);
         sv.load(Vb, ld, k0 + 2 * BN, T);
       }
-    }
-  }
-  if (qi < T)
-    store_T<HD>(dQ + ((int64_t)b * T + qi) * ld + (int64_t)head * HD, dq, scale, h, ROPE_OUT ? cosT : nullptr, sinT, qi);
-}
-
-// dQ, software-pipelined (round 3; q/k already rotated, T % 64 == 0): the per-32-key-half chain of
-// attn_bwd_dq_kernel (S / dP MFMAs -> dS = P (dP - delta) on the VALU -> dQ MFMAs) is skewed by one
-// half: step u issues the S / dP MFMAs of half u+1 beside the dS vector work of half u, then the dQ
-// MFMAs of half u.  K/V ring, look-ahead, compile-time LDS slots and the diagonal-only mask as in
-// attn_fwd_sp_kernel (wave of 32 queries: only its last 32-key half u = q0w / 32 is masked).  PRE: the
-// row statistics (delta, -delta, -LSE/c for the dK/dV kernel) as in attn_bwd_dq_kernel.
-template <int HD, bool ROPE_OUT, bool PRE, bool PAD, int LOOK>
-__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dq_sp_kernel(
-    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-    bf16_t* __restrict__ dQ, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
-    const float* __restrict__ cosT, const float* __restrict__ sinT, const bf16_t* __restrict__ O,
-    float* __restrict__ NL, float* __restrict__ ND, const int* __restrict__ KS, int order) {
-  constexpr int BN = 64, NT = HD / 16, NO = HD / 32, NS = LOOK + 2;
-  constexpr int TILE = BN * HD;
-  constexpr int PIECES = 2 * TileDma<HD, BN>::IPW;
-  __shared__ __attribute__((aligned(16))) bf16_t KV[NS * 2 * TILE];
-
-  const int nqb = (T + 127) / 128, bh_count = B * nh;
-  int qb, bh;
-  if (order) {  // see attn_fwd_kernel
-    const int rep = nh / nkv, grp = nqb * rep;
-    const int id = xcd_remap(blockIdx.x, nqb * bh_count);
-    const int gi = id / grp, wi = id % grp;
-    qb = nqb - 1 - wi / rep;
-    bh = (gi / nkv) * nh + (gi % nkv) * rep + wi % rep;
-  } else {
-    qb = nqb - 1 - (int)(blockIdx.x / bh_count);
-    bh = blockIdx.x % bh_count;
-  }
-  const int b = bh / nh, head = bh % nh, kvh = head / (nh / nkv);
-  const int ks = PAD ? KS[b] : 0;
-  const int lane = threadIdx.x & 63, h = lane >> 5, c32 = lane & 31;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4, i16 = lane & 15;
-  const int q0w = qb * 128 + w * 32, qi = q0w + c32;
-  const float c = scale * LOG2E;
-  const bf16_t* Qb = Q + (int64_t)b * T * ld + (int64_t)head * HD;
-  const bf16_t* dOb = dO + (int64_t)b * T * ldo + (int64_t)head * HD;
-  const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
-  const bf16_t* Vb = V + (int64_t)b * T * ld + (int64_t)kvh * HD;
-  const int ntiles = min(T, qb * 128 + 128) / BN;
-  const int uw = q0w < T ? q0w / 32 : -1;  // last (diagonal) 32-key half of this wave
-
-  TileDma<HD, BN> tdma;
-  tdma.init(ld);
-  const uint32_t kv_a = lds_addr(KV);
-  auto dma_issue = [&](int j, int sl) {
-    const uint32_t a = kv_a + (uint32_t)(sl * 2 * TILE * 2);
-    tdma.issue(Kb + (int64_t)j * BN * ld, a);
-    tdma.issue(Vb + (int64_t)j * BN * ld, a + TILE * 2);
-  };
-  for (int p = 0; p <= LOOK && p < ntiles; ++p) dma_issue(p, p);
-
-  // row operands (unpredicated: a row past T reads row T-1 and is never stored)
-  const int qr = min(qi, T - 1);
-  bf16x8 qf[NT], dof[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    qf[t] = load16(Qb + (int64_t)qr * ld + 16 * t + 8 * h);
-    dof[t] = load16(dOb + (int64_t)qr * ldo + 16 * t + 8 * h);
-  }
-  const int64_t rowstat = ((int64_t)b * nh + head) * T;
-  float lse = LSE[rowstat + qr];
-  float dlt;
-  if constexpr (PRE) {
-    float acc = 0.f;
-    const bf16_t* Orow = O + ((int64_t)b * T + qr) * ldo + (int64_t)head * HD;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const bf16x8 of = load16(Orow + 16 * t + 8 * h);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc = fmaf(bf2f((bf16_t)of[j]), bf2f((bf16_t)dof[t][j]), acc);
-    }
-    dlt = pair_sum32(acc);
-    if (qi < T && h == 0) {
-      ND[rowstat + qi] = -dlt;
-      NL[rowstat + qi] = -lse * (1.f / c);
-    }
-  } else {
-    dlt = DELTA[rowstat + qr];
-  }
-  f32x16 dq[NO];
-#pragma unroll
-  for (int o = 0; o < NO; ++o) dq[o] = f32x16{};
-
-  // S^T / dP^T of 32-key half KT of the tile in LDS slot SL
-  auto sdp = [&](f32x16& s, f32x16& dp, auto slot_t, auto kt_t) {
-    constexpr int SL = decltype(slot_t)::value, KT = decltype(kt_t)::value;
-    const bf16_t* kt_ = KV + SL * 2 * TILE;
-    const bf16_t* vt_ = kt_ + TILE;
-    s = f32x16{};
-    dp = f32x16{};
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      s = mfma32(row_frag<HD>(kt_, KT * 32 + c32, t, h), qf[t], s);
-      dp = mfma32(row_frag<HD>(vt_, KT * 32 + c32, t, h), dof[t], dp);
-    }
-  };
-  // dS = P (dP - delta) of half u, then dQ^T += K^T dS^T (K of slot SL, half KT)
-  auto ds_dq = [&](f32x16& s, f32x16& dp, int u, auto slot_t, auto kt_t, auto mask_t) {
-    constexpr int SL = decltype(slot_t)::value, KT = decltype(kt_t)::value;
-    constexpr bool MASK = decltype(mask_t)::value;
-    if constexpr (MASK) {  // select after the exp: a pad query row has lse = -inf
-      const int lim = qi - u * 32 - 4 * h, plim = ks - u * 32 - 4 * h;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ko = (r & 3) + 8 * (r >> 2);
-        const float p = (ko > lim || (PAD && ko < plim)) ? 0.f : fexp2(fmaf(s[r], c, -lse));
-        dp[r] = p * (dp[r] - dlt);
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dp[r] = fexp2(fmaf(s[r], c, -lse)) * (dp[r] - dlt);
-    }
-    const bf16_t* kt_ = KV + SL * 2 * TILE;
-#pragma unroll
-    for (int sidx = 0; sidx < 2; ++sidx) {
-      const bf16x8 dsf = pack_frag(dp, sidx);
-#pragma unroll
-      for (int o = 0; o < NO; ++o) dq[o] = mfma32(tr_frag<HD>(kt_, KT * 32 + 16 * sidx, o * 32, g, i16), dsf, dq[o]);
-    }
-  };
-
-  if (LOOK >= 2 && ntiles > 2) vm_wait<(LOOK >= 2 ? 2 * PIECES : 0)>();
-  else if (ntiles > 1) vm_wait<PIECES>();
-  else vm_wait<0>();
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    asm volatile("" : "+v"(qf[t]));
-    asm volatile("" : "+v"(dof[t]));
-  }
-  asm volatile("" : "+v"(lse), "+v"(dlt));
-  __syncthreads();
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using TT = std::true_type;
-  using FF = std::false_type;
-  f32x16 s, dp;
-  sdp(s, dp, I0{}, I0{});
-
-  auto iter = [&](int j, auto slot_t) {
-    constexpr int SL = decltype(slot_t)::value;
-    using SN = std::integral_constant<int, (SL + 1) % NS>;
-    if (j + 1 < ntiles) {
-      if (LOOK >= 2 && j + 2 < ntiles) vm_wait<(LOOK >= 2 ? PIECES : 0)>();
-      else vm_wait<0>();
-    }
-    __syncthreads();
-    if (j + LOOK + 1 < ntiles) dma_issue(j + LOOK + 1, (SL + LOOK + 1) % NS);
-    // half 2j (next: half 2j+1, same tile)
-    const int u0 = 2 * j;
-    if (u0 < uw) {
-      f32x16 s2, dp2;
-      sdp(s2, dp2, slot_t, I1{});
-      if (PAD && u0 * 32 < ks) ds_dq(s, dp, u0, slot_t, I0{}, TT{});
-      else ds_dq(s, dp, u0, slot_t, I0{}, FF{});
-      s = s2;
-      dp = dp2;
-    } else if (u0 == uw) {
-      ds_dq(s, dp, u0, slot_t, I0{}, TT{});
-    }
-    // half 2j+1 (next: half 2j+2 = first half of tile j+1, landed at this iteration's barrier)
-    const int u1 = 2 * j + 1;
-    if (u1 < uw) {
-      f32x16 s2, dp2;
-      sdp(s2, dp2, SN{}, I0{});
-      if (PAD && u1 * 32 < ks) ds_dq(s, dp, u1, slot_t, I1{}, TT{});
-      else ds_dq(s, dp, u1, slot_t, I1{}, FF{});
-      s = s2;
-      dp = dp2;
-    } else if (u1 == uw) {
-      ds_dq(s, dp, u1, slot_t, I1{}, TT{});
-    }
-  };
-  for (int j = 0; j < ntiles; j += NS) {
-    iter(j, I0{});
-    if (j + 1 < ntiles) iter(j + 1, I1{});
-    if (j + 2 < ntiles) iter(j + 2, std::integral_constant<int, 2>{});
-    if constexpr (NS > 3) {
-      if (j + 3 < ntiles) iter(j + 3, std::integral_constant<int, 3 % NS>{});
     }
   }
   if (qi < T)
@@ -1293,22 +926,10 @@ static int fwd_launch(const void* q, const void* k, const void* v, void* o, floa
   // deferred-max threshold (log2 units; ND_ATTN_THR for A/B, 0 = move the max on every increase)
   const char* te = getenv("ND_ATTN_THR");
   const float thr = te ? (float)atof(te) : 8.f;
-  // ND_ATTN_FWD: 'r' register-staged, 's' the pipelined kernel (ND_ATTN_LOOK = DMA look-ahead in
-  // tiles, 1 or 2; measured 0.89x, not the default), else the LDS-DMA kernel
+  // ND_ATTN_FWD: 'r' register-staged, else the LDS-DMA kernel (ND_ATTN_FWD_W=8: 256-query blocks,
+  // ND_ATTN_ABL: ablation / variant bits; profiles/r3_attention_experiments.md)
   const char* fe = getenv("ND_ATTN_FWD");
   const char fv = fe ? fe[0] : 'd';
-  if constexpr (HD <= 64) {
-    if (!cosT && T % 64 == 0 && fv == 's') {
-      const char* le = getenv("ND_ATTN_LOOK");
-      if (le && le[0] == '2')
-        hipLaunchKernelGGL((attn_fwd_sp_kernel<HD, PAD, 2>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k,
-                           (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, ks, thr, attn_order());
-      else
-        hipLaunchKernelGGL((attn_fwd_sp_kernel<HD, PAD, 1>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k,
-                           (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, ks, thr, attn_order());
-      ND_LAUNCH_CHECK();
-    }
-  }
   if (cosT)
     hipLaunchKernelGGL((attn_fwd_kernel<HD, true, false, PAD>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr, attn_order());
@@ -1321,9 +942,28 @@ static int fwd_launch(const void* q, const void* k, const void* v, void* o, floa
                        (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr,      \
                        attn_order());                                                                              \
     break;
-    switch (PAD ? 0 : abl) {
-      ND_ABL(1) ND_ABL(2) ND_ABL(3) ND_ABL(4) ND_ABL(7) ND_ABL(8) ND_ABL(12) ND_ABL(16) ND_ABL(20) ND_ABL(24) ND_ABL(28)
-      default: ND_ABL(0)
+    const char* we = getenv("ND_ATTN_FWD_W");
+    bool w8 = false;
+    if constexpr (HD >= 64) w8 = we && we[0] == '8';  // HD 32: a 64-row tile is 4 DMA pieces, < 8 waves
+    if (w8) {
+      const dim3 g8((T + 255) / 256 * B * nh), b8(512);
+      switch (PAD ? 0 : abl) {
+#define ND_ABL8(A)                                                                                                   \
+  case A:                                                                                                            \
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, false, true, PAD, A, 8>), g8, b8, 0, s, (const bf16_t*)q, (const bf16_t*)k, \
+                       (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr,        \
+                       attn_order());                                                                                \
+    break;
+        ND_ABL8(1) ND_ABL8(3) ND_ABL8(4) ND_ABL8(28) ND_ABL8(32)
+        default: ND_ABL8(0)
+#undef ND_ABL8
+      }
+    } else {
+      switch (PAD ? 0 : abl) {
+        ND_ABL(1) ND_ABL(2) ND_ABL(3) ND_ABL(4) ND_ABL(7) ND_ABL(8) ND_ABL(12) ND_ABL(16) ND_ABL(20) ND_ABL(24) ND_ABL(28)
+        ND_ABL(32)
+        default: ND_ABL(0)
+      }
     }
 #undef ND_ABL
   }
@@ -1390,8 +1030,9 @@ __global__ void __launch_bounds__(256) attn_neg_stats_kernel(const float* __rest
   }
 }
 
-template <int HD, bool ROPE_OUT, int BQ = 64, bool PAD = false>
-__global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_kernel(
+// NW: waves per workgroup (8 = 256-key blocks: every Q / dO tile DMA'd once per 256 keys)
+template <int HD, bool ROPE_OUT, int BQ = 64, bool PAD = false, int NW = 4>
+__global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ NL, const float* __restrict__ ND, bf16_t* __restrict__ dK,
     bf16_t* __restrict__ dV, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
@@ -1399,13 +1040,14 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
   constexpr int NT = HD / 16, NO = HD / 32;
   constexpr int CPR = HD / 8;              // 16-B chunks per row
   constexpr int RPI = 64 / CPR;            // rows per 1-KiB DMA wave-instruction
-  constexpr int IPW = (BQ / RPI) / 4;      // DMA instructions per wave per operand tile
+  constexpr int IPW = (BQ / RPI) / NW;     // DMA instructions per wave per operand tile
+  constexpr int KB = 32 * NW;              // keys per workgroup
   __shared__ __attribute__((aligned(16))) bf16_t Qs[2 * BQ * HD];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[2 * BQ * HD];
   __shared__ __attribute__((aligned(16))) float lse_s[2 * BQ];
   __shared__ __attribute__((aligned(16))) float del_s[2 * BQ];
 
-  const int bk_count = B * nkv, rep = nh / nkv, nkb = (T + 127) / 128;
+  const int bk_count = B * nkv, rep = nh / nkv, nkb = (T + KB - 1) / KB;
   int kb, bk;  // see attn_bwd_dkdv_kernel
   if (order) {
     const int id = xcd_remap(blockIdx.x, nkb * bk_count);
@@ -1419,7 +1061,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
   const int ks = PAD ? KS[b] : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15;
-  const int kw0 = kb * 128 + w * 32, key = kw0 + c32;
+  const int kw0 = kb * KB + w * 32, key = kw0 + c32;
   const float c = scale * LOG2E;
   const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
   const bf16_t* Vb = V + (int64_t)b * T * ld + (int64_t)kvh * HD;
@@ -1440,14 +1082,14 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
   uint32_t vq[IPW], vd[IPW];
 #pragma unroll
   for (int i = 0; i < IPW; ++i) {
-    const int row = (wu + 4 * i) * RPI + lane / CPR, p = lane % CPR;
+    const int row = (wu + NW * i) * RPI + lane / CPR, p = lane % CPR;
     const int lch = (soff<HD>(row, p * 8) - row * HD) / 8;  // soff maps logical -> physical; XOR: same map back
     vq[i] = (uint32_t)(((int64_t)row * ld + lch * 8) * 2);
     vd[i] = (uint32_t)(((int64_t)row * ldo + lch * 8) * 2);
   }
   const uint32_t qs_a = lds_addr(Qs), do_a = lds_addr(dOs), ls_a = lds_addr(lse_s), ds_a = lds_addr(del_s);
 
-  const int qstart = (kb * 128) / BQ * BQ;
+  const int qstart = (kb * KB) / BQ * BQ;
   const int ntq = (T - qstart + BQ - 1) / BQ;
   const int nit = ntq * rep;
   auto issue = [&](int it) {
@@ -1458,7 +1100,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_ke
     const bf16_t* sd = dO + ((int64_t)b * T + q0) * ldo + (int64_t)head * HD;
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
-      const uint32_t off = (uint32_t)(buf * BQ * HD * 2 + (wu + 4 * i) * 1024);
+      const uint32_t off = (uint32_t)(buf * BQ * HD * 2 + (wu + NW * i) * 1024);
       adma_b128(sq, vq[i], qs_a + off);
       adma_b128(sd, vd[i], do_a + off);
     }
@@ -1635,23 +1277,14 @@ static int bwd_fused_launch(const void* q, const void* k, const void* v, const v
   const int nb = (T + 127) / 128;
   const int64_t n = (int64_t)B * nh * T;
   float *nl = ws, *nd = ws + n;
-  // ND_ATTN_DQ: 's' = the pipelined dQ kernel (HD <= 64; ND_ATTN_LOOK as the forward; measured 0.97x,
-  // not the default), else attn_bwd_dq_kernel
-  const char* qe = getenv("ND_ATTN_DQ");
-  const char* le = getenv("ND_ATTN_LOOK");
   bool done = false;
-  if constexpr (HD <= 64) {
-    if (qe && qe[0] == 's') {
-      if (le && le[0] == '2')
-        hipLaunchKernelGGL((attn_bwd_dq_sp_kernel<HD, ROPE_OUT, true, PAD, 2>), dim3(nb * B * nh), dim3(256), 0, s,
-                           (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
-                           (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks,
-                           attn_order());
-      else
-        hipLaunchKernelGGL((attn_bwd_dq_sp_kernel<HD, ROPE_OUT, true, PAD, 1>), dim3(nb * B * nh), dim3(256), 0, s,
-                           (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
-                           (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks,
-                           attn_order());
+  if constexpr (HD >= 64) {  // ND_ATTN_DQ_W=8: 256-query blocks
+    const char* we = getenv("ND_ATTN_DQ_W");
+    if (!done && we && we[0] == '8') {
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, ROPE_OUT, true, true, PAD, 8>), dim3((T + 255) / 256 * B * nh),
+                         dim3(512), 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
+                         lse, nullptr, (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd,
+                         ks, attn_order());
       done = true;
     }
   }
@@ -1659,7 +1292,14 @@ static int bwd_fused_launch(const void* q, const void* k, const void* v, const v
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, ROPE_OUT, true, true, PAD>), dim3(nb * B * nh), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
                        (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks, attn_order());
-  if (T % 128 == 0)
+  const char* kwe = getenv("ND_ATTN_DKDV_W");
+  bool kw8 = false;
+  if constexpr (HD >= 64) kw8 = kwe && kwe[0] == '8' && T % 128 == 0;
+  if (kw8)  // 256-key blocks
+    hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD, 8>), dim3((T + 255) / 256 * B * nkv), dim3(512),
+                       0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
+                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
+  else if (T % 128 == 0)
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
                        (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));

@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Attention forward kernel A/B on the bench shapes (pre-rotated q|k, the fused-RoPE path): variants are
-ND_ATTN_FWD[+ND_ATTN_LOOK] pairs, e.g. d (round-2 LDS-DMA kernel), s1 / s2 (pipelined, 1- / 2-tile
-look-ahead).  CUDA-event timing, interleaved rounds, median.
+"""Attention kernel A/B on the bench shapes (pre-rotated q|k, the fused-RoPE path); CUDA-event timing,
+5 interleaved rounds, median.  Forward variants: d (LDS-DMA kernel, 128-query blocks), d8 (256-query
+blocks), r (register-staged), with an optional ':<bits>' ND_ATTN_ABL suffix (ablations, or 32 = the
+cheaper-mask variant).  Fused-backward variants: o (default), o8 (256-query dQ blocks), k8 (256-key dK/dV
+blocks).  Results: profiles/r3_attention_experiments.md.
 
-    VARIANTS=d,s1,s2 python scripts/attn_fwd_ab.py
+    VARIANTS=d,d:32,d8 BWD_VARIANTS=o,o8,k8 python scripts/attn_fwd_ab.py   (FWD_ONLY=1: skip the backward)
 """
 import os
 import sys
@@ -26,8 +28,20 @@ def timed(fn, iters=10):
     return s.elapsed_time(e) / iters * 1e3
 
 
-variants = os.environ.get("VARIANTS", "d,s1,s2").split(",")
-bwd_variants = os.environ.get("BWD_VARIANTS", "o,s1,s2").split(",")  # ND_ATTN_DQ[+ND_ATTN_LOOK]
+def set_fwd(var):
+    vv, _, abl = var.partition(":")
+    os.environ["ND_ATTN_FWD"] = vv[0]
+    os.environ["ND_ATTN_FWD_W"] = vv[1:] or "4"
+    os.environ["ND_ATTN_ABL"] = abl or "0"
+
+
+def set_bwd(var):
+    os.environ["ND_ATTN_DQ_W"] = "8" if var == "o8" else "4"
+    os.environ["ND_ATTN_DKDV_W"] = "8" if var == "k8" else "4"
+
+
+variants = os.environ.get("VARIANTS", "d,d:32,d8").split(",")
+bwd_variants = os.environ.get("BWD_VARIANTS", "o,o8,k8").split(",")
 L = _ext.lib()
 for (B, T, nh, nkv, hd) in [(64, 1024, 16, 16, 64), (16, 1024, 32, 4, 64), (16, 2048, 16, 16, 64)]:
     ld = (nh + 2 * nkv) * hd
@@ -41,14 +55,10 @@ for (B, T, nh, nkv, hd) in [(64, 1024, 16, 16, 64), (16, 1024, 32, 4, 64), (16, 
         _ext.check(L.nd_attn_fwd_ks(qkv.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(), B, nh,
                                     nkv, T, hd, ld, nh * hd, 0, 0, hd ** -0.5, 0, st), "fwd")
     flops = 4.0 * B * nh * T * T * hd / 2
-    res = {}
-    outs = {}
+    res, outs = {}, {}
     for rnd in range(5):
         for var in variants:
-            vv, _, abl = var.partition(":")  # "d:3" = round-2 kernel with ablation 3 (ND_ATTN_ABL)
-            os.environ["ND_ATTN_FWD"] = vv[0]
-            os.environ["ND_ATTN_LOOK"] = vv[1:] or "1"
-            os.environ["ND_ATTN_ABL"] = abl or "0"
+            set_fwd(var)
             res.setdefault(var, []).append(timed(run))
             if rnd == 0:
                 outs[var] = o.clone()
@@ -59,10 +69,9 @@ for (B, T, nh, nkv, hd) in [(64, 1024, 16, 16, 64), (16, 1024, 32, 4, 64), (16, 
         d = ((outs[var].float() - base).norm() / base.norm()).item()
         line += f"  {var} {t:7.1f} us {flops / t / 1e6:5.0f} TF (diff {d:.1e})"
     print(line, flush=True)
-    # fused backward (dQ + row statistics, then dK/dV): the dQ-kernel variants
-    os.environ["ND_ATTN_FWD"], os.environ["ND_ATTN_LOOK"], os.environ["ND_ATTN_ABL"] = "d", "1", "0"
     if os.environ.get("FWD_ONLY"):
         continue
+    set_fwd("d")
     run()
     do = torch.randn(B * T, nh * hd, device="cuda").bfloat16()
     dqkv = torch.empty_like(qkv)
@@ -76,13 +85,13 @@ for (B, T, nh, nkv, hd) in [(64, 1024, 16, 16, 64), (16, 1024, 32, 4, 64), (16, 
     res, outs = {}, {}
     for rnd in range(5):
         for var in bwd_variants:
-            os.environ["ND_ATTN_DQ"] = var[0]
-            os.environ["ND_ATTN_LOOK"] = var[1:] or "1"
+            set_bwd(var)
             res.setdefault(var, []).append(timed(bwd))
             if rnd == 0:
                 outs[var] = dqkv.clone()
+    set_bwd("o")
     base = outs[bwd_variants[0]].float()
-    line = f"  bwd (dQ variants):"
+    line = "  fused bwd:"
     for var in bwd_variants:
         t = sorted(res[var])[2]
         d = ((outs[var].float() - base).norm() / base.norm()).item()

@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """A few launches of the attention forward / fused backward kernels at the Llama-150M bench shape
-(B=64, T=1024, 16x64, pre-rotated q|k) for rocprofv3 --pmc: forward variants d (round 2) and s (pipelined),
-dQ variants o (round 2) and s (pipelined); kernel names tell them apart in the counter CSV.
+(B=64, T=1024, 16x64, pre-rotated q|k) for rocprofv3 --pmc.
 
     python scripts/attn_pmc.py [--iters 3]
 """
@@ -31,12 +30,11 @@ dk, dv = dqkv[:, nh * hd:], dqkv[:, (nh + nkv) * hd:]
 ws = torch.empty(2, B, nh, T, device="cuda")
 st = _ext.stream_ptr(qkv.device)
 for _ in range(a.iters):
-    for fv in ("d", "s"):
+    for fv in ("d",):
         os.environ["ND_ATTN_FWD"] = fv
         _ext.check(L.nd_attn_fwd_ks(qkv.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(), B, nh,
                                     nkv, T, hd, ld, nh * hd, 0, 0, hd ** -0.5, 0, st), "fwd")
-    for qv in ("o", "s"):
-        os.environ["ND_ATTN_DQ"] = qv
+    for qv in ("o",):
         _ext.check(L.nd_attn_bwd_fused_ks(qkv.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(),
                                           lse.data_ptr(), dqkv.data_ptr(), dk.data_ptr(), dv.data_ptr(), ws.data_ptr(),
                                           B, nh, nkv, T, hd, ld, nh * hd, 0, 0, hd ** -0.5, 0, 0, st), "bwd")

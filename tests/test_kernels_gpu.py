@@ -520,15 +520,18 @@ def _store_view(store, flat, name):
     (2, 64, 2, 2, 64, None), (2, 192, 4, 2, 64, None), (1, 1024, 4, 4, 64, None), (3, 512, 8, 2, 64, None),
     (2, 320, 4, 4, 32, None), (2, 256, 4, 4, 64, (0, 100)), (2, 1024, 16, 16, 64, (0, 700)),
 ])
-@pytest.mark.parametrize("variant", ["s1", "s2", "d", "r"])
+@pytest.mark.parametrize("variant", ["d", "d8", "dx", "d8x", "r"])
 def test_attention_fwd_variants(B, T, nh, nkv, hd, pads, variant, monkeypatch):
-    """Forward kernels on pre-rotated q|k (the fused-RoPE path): the software-pipelined kernel with a
-    1- and 2-tile K/V look-ahead (default 's1') and the round-2 LDS-DMA kernel ('d') against fp32
-    torch, output and log-sum-exp; T % 128 == 64 leaves idle waves in the last query block."""
+    """Forward kernels on pre-rotated q|k (the fused-RoPE path): the LDS-DMA kernel with 128- and
+    256-query blocks ('d', 'd8'; 'x' = its cheaper-mask / split-sum variant) and the register-staged
+    one ('r') against fp32 torch, output and log-sum-exp; T % 128 == 64 leaves idle waves in the last
+    query block."""
     from nanodiloco_amd.ops import _ext
     from nanodiloco_amd.ops.attention import key_start
+    monkeypatch.setenv("ND_ATTN_ABL", "32" if variant.endswith("x") else "0")  # x: the ILP softmax variant
+    variant = variant.rstrip("x")
     monkeypatch.setenv("ND_ATTN_FWD", variant[0])
-    monkeypatch.setenv("ND_ATTN_LOOK", variant[1:] or "1")
+    monkeypatch.setenv("ND_ATTN_FWD_W", variant[1:] if variant[0] == "d" and variant[1:] else "4")
     ld = (nh + 2 * nkv) * hd
     qkv = torch.randn(B * T, ld, device=DEV).bfloat16()
     qkv[T // 2, nh * hd:(nh + 1) * hd] *= 20  # a late key with a large score: deferred-max rescale path
@@ -570,13 +573,13 @@ def test_attention_fwd_variants(B, T, nh, nkv, hd, pads, variant, monkeypatch):
     (2, 64, 2, 2, 64, None), (2, 192, 4, 2, 64, None), (1, 1024, 4, 4, 64, None), (2, 320, 4, 4, 32, None),
     (2, 256, 4, 4, 64, (0, 100)), (2, 1024, 8, 2, 64, (0, 700)),
 ])
-@pytest.mark.parametrize("variant", ["s1", "s2", "o"])
+@pytest.mark.parametrize("variant", ["o", "o8", "k8"])
 def test_attention_bwd_dq_variants(B, T, nh, nkv, hd, pads, variant, monkeypatch):
-    """Fused backward (dQ kernel with the row statistics, then dK/dV) with the software-pipelined dQ
-    kernel (1- / 2-tile look-ahead) and the round-2 one ('o'): all three gradients against fp32."""
+    """Fused backward (dQ kernel with the row statistics, then dK/dV) with 128- / 256-query dQ blocks
+    ('o', 'o8') and 256-key dK/dV blocks ('k8'): all three gradients against fp32."""
     from nanodiloco_amd.ops.attention import key_start, rope_cache
-    monkeypatch.setenv("ND_ATTN_DQ", variant[0])
-    monkeypatch.setenv("ND_ATTN_LOOK", variant[1:] or "1")
+    monkeypatch.setenv("ND_ATTN_DQ_W", variant[1:] if variant[0] == "o" and variant[1:] else "4")
+    monkeypatch.setenv("ND_ATTN_DKDV_W", "8" if variant == "k8" else "4")  # 256-key dK/dV blocks
     ld = (nh + 2 * nkv) * hd
     ks = None
     if pads is not None:
