@@ -82,6 +82,9 @@ struct PPEpi {
 
 // stores per wave per tile epilogue (counted by the vmcnt waits that follow it)
 template <int EPI> struct NStores { static constexpr int v = EPI == PP_SWIGLU ? 24 : EPI == PP_DSWIGLU ? 32 : 16; };
+#ifndef DSW_PF
+#define DSW_PF 6  // PP_DSWIGLU epilogue: gate / up load steps in flight
+#endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
@@ -270,6 +273,25 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
     } else {  // PP_DSWIGLU: acc = d(act)[m][f]; C = d(gate | up) [M, 2N]
       const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
       const auto gr = rsrc(ep.gu + (int64_t)m0 * ep.ld_gu, (uint32_t)((int64_t)rows * ep.ld_gu * 2));
+      // the 16 (row block, column pair) steps read gate / up from HBM: their loads run PF steps ahead
+      // (2 x PF x 4 VGPRs, taken from the next K-tile's fragment registers, free here) instead of one
+      // -- one exposed HBM round trip per tile instead of per step
+      constexpr int PF = DSW_PF;
+      u32x4 gq[PF], uq[PF];
+      auto gu_off = [&](int st, int half) -> uint32_t {
+        const int a = st >> 1, bp = st & 1;
+        const int mr = g * 128 + a * 16 + r16;
+        const int f = n0 + wn * 64 + (2 * bp + (q & 1)) * 16 + (q >> 1) * 8;
+        // branch-free select (a ?: here becomes two exec-masked copies of the load)
+        const uint32_t okm = 0u - (uint32_t)(f < N);
+        return ((uint32_t)(((int64_t)mr * ep.ld_gu + half * N + f) * 2) & okm) | (0x80000000u & ~okm);
+      };
+#pragma unroll
+      for (int st = 0; st < PF; ++st) {
+        gq[st] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st, 0), 0, 0);
+        uq[st] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st, 1), 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch above the first use (the scheduler sinks it)
 #pragma unroll
       for (int a = 0; a < 8; ++a) {
         const int mr = g * 128 + a * 16 + r16;
@@ -278,10 +300,13 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
           // after the pair swap this lane holds d(act) of 8 consecutive units f .. f + 7
           const int f = n0 + wn * 64 + (2 * bp + (q & 1)) * 16 + (q >> 1) * 8;
           const bool ok = f < N;
-          const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ep.ld_gu + f) * 2) : 0x80000000u;
-          const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ep.ld_gu + N + f) * 2) : 0x80000000u;
-          const u32x4 gv = __builtin_amdgcn_raw_buffer_load_b128(gr, og, 0, 0);
-          const u32x4 uv = __builtin_amdgcn_raw_buffer_load_b128(gr, ou, 0, 0);
+          const int st = 2 * a + bp;
+          const u32x4 gv = gq[st % PF], uv = uq[st % PF];
+          if (st + PF < 16) {
+            gq[st % PF] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st + PF, 0), 0, 0);
+            uq[st % PF] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st + PF, 1), 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
           // d(act) as fp32 in the same 8-unit order: swap the fp32 quads like pair16 does
           f32x4 d0, d1;
 #pragma unroll

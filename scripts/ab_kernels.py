@@ -10,6 +10,7 @@ compared inside one process, alternating).
               are not needed: each op is timed with HIP events, min over rounds)
 --what step : one full forward+backward of Llama-150M (micro-batch 32 x 1024)
 --what wgrad: the wgrad GEMM shapes
+--what epi  : the fused-epilogue ping-pong GEMMs (q|k|v+RoPE, gate|up+SwiGLU, down dgrad+SwiGLU bwd)
 """
 import argparse
 import os
@@ -67,6 +68,18 @@ def workloads(what):
             _ext.check(_ext.lib().nd_ce_fwd_bwd(logits.data_ptr(), 1, tgt.data_ptr(), loss.data_ptr(), sc.data_ptr(),
                                                 n, V, -100, 0, 0, 0.0, _ext.stream_ptr()), "ce")
         out["ce_16k"] = ce
+    elif what == "epi":  # the fused-epilogue ping-pong GEMMs at the Llama-150M bench shapes
+        from nanodiloco_amd.ops import gemm as G
+        M, d, F = 65536, 1024, 2688
+        x = (torch.randn(M, d, device="cuda") * 0.5).bfloat16()
+        wq = (torch.randn(3 * d, d, device="cuda") * 0.05).bfloat16()
+        wgu = (torch.randn(2 * F, d, device="cuda") * 0.05).bfloat16()
+        wdt = (torch.randn(F, d, device="cuda") * 0.05).bfloat16()
+        cos, sin = rope_cache(1024, 64, 10000.0, None, "cuda")
+        gu = torch.randn(M, 2 * F, device="cuda").bfloat16()
+        out["rope"] = lambda: G.gemm_pp_rope(x, wq, cos, sin, 1024, 64, 2 * d)
+        out["swiglu"] = lambda: G.gemm_pp_swiglu(x, wgu)
+        out["dswiglu"] = lambda: G.gemm_pp_dswiglu(x, wdt, gu)
     elif what == "wgrad":
         from nanodiloco_amd.ops.gemm import wgrad
         for name, (M, N) in {"qkv": (3072, 1024), "o": (1024, 1024), "gate_up": (5376, 1024),
@@ -81,7 +94,7 @@ def workloads(what):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--alt", required=True)
-    ap.add_argument("--what", default="attn", choices=["attn", "step", "wgrad", "ce"])
+    ap.add_argument("--what", default="attn", choices=["attn", "step", "wgrad", "ce", "epi"])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()

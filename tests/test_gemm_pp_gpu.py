@@ -40,7 +40,11 @@ def maxrel(a, b):
 SHAPES = [(256, 256, 64), (512, 768, 128), (300, 264, 192), (1000, 520, 640), (4096, 3072, 1024),
           (2048, 2688, 1024), (8192, 1024, 5376), (64, 8, 64),
           # several tiles per persistent workgroup (the epilogue inside the next tile's first phase)
-          (16384, 3072, 1024), (32768, 2688, 256), (9000, 1000, 320), (70000 // 8 * 8, 1032, 128)]
+          (16384, 3072, 1024), (32768, 2688, 256), (9000, 1000, 320), (70000 // 8 * 8, 1032, 128),
+          # Llama-150M lm head logits / dgrad, and the Llama-1B plain projections (o / down fwd, q|k|v,
+          # o and gate|up dgrad, lm head) at reduced M
+          (2048, 32000, 1024), (2048, 1024, 32000), (2048, 2048, 2048), (2048, 2048, 5632), (2048, 2048, 2560),
+          (1024, 2048, 11264), (1024, 32000, 2048), (1024, 2048, 32000)]
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
@@ -82,7 +86,8 @@ def test_gemm_pp_identity_asymmetric():
 
 
 @pytest.mark.parametrize("B,T,nh,nkv,hd", [(2, 512, 16, 16, 64), (1, 1024, 8, 2, 64), (3, 128, 4, 4, 32),
-                                           (2, 256, 8, 2, 32), (8, 1024, 16, 16, 64)])
+                                           (2, 256, 8, 2, 32), (8, 1024, 16, 16, 64),
+                                           (2, 1024, 32, 4, 64)])  # Llama-1B q|k|v (N = 2560)
 def test_gemm_pp_rope(B, T, nh, nkv, hd):
     K = 256
     N = (nh + 2 * nkv) * hd
@@ -101,7 +106,8 @@ def test_gemm_pp_rope(B, T, nh, nkv, hd):
     assert maxrel(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("M,F,K", [(1024, 672, 1024), (4096, 2688, 1024), (300, 136, 128), (20000, 1408, 256)])
+@pytest.mark.parametrize("M,F,K", [(1024, 672, 1024), (4096, 2688, 1024), (300, 136, 128), (20000, 1408, 256),
+                                   (2048, 5632, 2048)])  # Llama-1B gate|up
 def test_gemm_pp_swiglu(M, F, K):
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(2 * F, K, device=DEV) * 0.05).bfloat16()
@@ -112,7 +118,8 @@ def test_gemm_pp_swiglu(M, F, K):
     assert rel(act, torch.nn.functional.silu(g) * u) < 5e-3
 
 
-@pytest.mark.parametrize("M,F,K", [(1024, 672, 1024), (4096, 2688, 1024), (300, 136, 128), (20000, 1408, 256)])
+@pytest.mark.parametrize("M,F,K", [(1024, 672, 1024), (4096, 2688, 1024), (300, 136, 128), (20000, 1408, 256),
+                                   (2048, 5632, 2048)])  # Llama-1B down dgrad
 def test_gemm_pp_dswiglu(M, F, K):
     gu = torch.randn(M, 2 * F, device=DEV).bfloat16()
     dy = torch.randn(M, K, device=DEV).bfloat16()

@@ -253,7 +253,9 @@ def test_outer_nesterov_matches_torch_sgd(comm):
 
 # ----------------------------------------------------------------------------------- wgrad GEMM
 @pytest.mark.parametrize("M,N,K", [(3072, 1024, 4096), (1024, 1024, 32768), (1000, 264, 777), (32000, 1024, 2048),
-                                   (128, 512, 64), (5376, 1024, 65536), (1024, 2688, 16640)])
+                                   (128, 512, 64), (5376, 1024, 65536), (1024, 2688, 16640),
+                                   # Llama-1B: q|k|v, gate|up, down, lm head
+                                   (2560, 2048, 8192), (11264, 2048, 4096), (2048, 5632, 4096), (32000, 2048, 2048)])
 @pytest.mark.parametrize("variant", ["", "reg", "dma0", "4w"])
 def test_wgrad_gemm(M, N, K, variant, monkeypatch):
     monkeypatch.setenv("ND_WGRAD_VARIANT", variant)
