@@ -331,10 +331,34 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
           }
           const u32x4 og4 = u32x4{pack2(dg[0], dg[1]), pack2(dg[2], dg[3]), pack2(dg[4], dg[5]), pack2(dg[6], dg[7])};
           const u32x4 ou4 = u32x4{pack2(du[0], du[1]), pack2(du[2], du[3]), pack2(du[4], du[5]), pack2(du[6], du[7])};
-          const uint32_t cg = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
-          const uint32_t cu = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
-          __builtin_amdgcn_raw_buffer_store_b128(og4, cr, cg, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(ou4, cr, cu, 0, 0);
+          if constexpr ((ABL & 256) == 0) {
+            // full-line stores as in the plain epilogue: d(gate) rows 0-15 and d(up) rows 16-31 of the
+            // wave's 4-KiB LDS staging region; after both column halves, 16 rows x 128 B per output
+            char* stg = smem + 2 * BUF_B + w * 4096;
+            const int ch = (2 * bp + (q & 1)) * 2 + (q >> 1);
+            *reinterpret_cast<u32x4*>(stg + r16 * 128 + ((ch ^ (r16 & 7)) << 4)) = og4;
+            *reinterpret_cast<u32x4*>(stg + (16 + r16) * 128 + ((ch ^ (r16 & 7)) << 4)) = ou4;
+            if (bp == 1) {
+              asm volatile("" ::: "memory");
+              const int lc = (lane + z) & 7;
+              const int col = n0 + wn * 64 + lc * 8;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int rr = i * 8 + ((lane + z) >> 3);  // staging row: i < 2 gate, else up
+                const u32x4 d = *reinterpret_cast<const u32x4*>(stg + rr * 128 + ((lc ^ (rr & 7)) << 4));
+                const int grow = g * 128 + a * 16 + (rr & 15);
+                const uint32_t off =
+                    col < N ? (uint32_t)(((int64_t)grow * ldc + (i >= 2 ? N : 0) + col) * 2) : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b128(d, cr, off, 0, STP);
+              }
+              asm volatile("" ::: "memory");
+            }
+          } else {
+            const uint32_t cg = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
+            const uint32_t cu = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b128(og4, cr, cg, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(ou4, cr, cu, 0, 0);
+          }
         }
       }
     }
