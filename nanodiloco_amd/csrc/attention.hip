@@ -332,7 +332,7 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
 // correct variant (cheaper mask, max tree, split row sum: needs T % 64 == 0).
 // NW: waves per workgroup (4 or 8; 8 = 256-query blocks, every K/V tile DMA'd once per 256 queries: DMA only)
 template <int HD, bool ROPE, bool DMA = false, bool PAD = false, int ABL = 0, int NW = 4>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
-__global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+__global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA) ? 4 : 3)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int nh, int nkv, int T,
                                                           int64_t ld, int64_t ldo, float scale,
@@ -405,10 +405,16 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(
       sv.load(Vb, ld, BN, T);
     }
   }
-  for (int j = 0; j < ntiles; ++j) {
+  // the tile loop is unrolled by the double-buffer parity (PAR = j & 1 at compile time): every LDS
+  // fragment address is then a per-lane base plus an immediate offset, no per-tile address VALU
+  auto tile = [&](int j, auto par_t) {
+    int par_v;  // compile-time for the LDS-DMA loop, j & 1 for the register-staged one
+    if constexpr (std::is_integral<decltype(par_t)>::value) par_v = par_t;
+    else par_v = decltype(par_t)::value;
+    const int PAR = par_v;
     const int k0 = j * BN;
-    const bf16_t* Kt = Ks + (j & 1) * (BN * HD);
-    const bf16_t* Vt = Vs + (j & 1) * (BN * HD);
+    const bf16_t* Kt = Ks + PAR * (BN * HD);
+    const bf16_t* Vt = Vs + PAR * (BN * HD);
     if constexpr (DMA) {
       if constexpr (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if constexpr (!(ABL & 2)) __syncthreads();
@@ -444,7 +450,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(
               else oacc[o] = mfma32(tr_frag<HD>(Vt, kt * 32 + 16 * sidx, o * 32, g, i16), pf, oacc[o]);
             }
           }
-        continue;
+        return;
       }
       float mx;
       if constexpr (ABL & 32) {
@@ -528,8 +534,8 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(
     }
     if constexpr (!DMA) {
       if (j + 1 < ntiles) {
-        sk.store(Ks + ((j + 1) & 1) * (BN * HD));
-        sv.store(Vs + ((j + 1) & 1) * (BN * HD));
+        sk.store(Ks + (PAR ^ 1) * (BN * HD));
+        sv.store(Vs + (PAR ^ 1) * (BN * HD));
       }
       __syncthreads();
       if (j + 2 < ntiles) {
@@ -537,6 +543,14 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 3)) attn_fwd_kernel(
         sv.load(Vb, ld, k0 + 2 * BN, T);
       }
     }
+    };
+  if constexpr (DMA) {
+    for (int j = 0; j < ntiles; j += 2) {
+      tile(j, std::integral_constant<int, 0>{});
+      if (j + 1 < ntiles) tile(j + 1, std::integral_constant<int, 1>{});
+    }
+  } else {
+    for (int j = 0; j < ntiles; ++j) tile(j, j & 1);
   }
   const float lt = pair_sum32(l);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;

@@ -68,6 +68,29 @@ def workloads(what):
             _ext.check(_ext.lib().nd_ce_fwd_bwd(logits.data_ptr(), 1, tgt.data_ptr(), loss.data_ptr(), sc.data_ptr(),
                                                 n, V, -100, 0, 0, 0.0, _ext.stream_ptr()), "ce")
         out["ce_16k"] = ce
+    elif what == "attnk":  # the raw attention kernels at the Llama-150M bench shape (pre-rotated q|k)
+        B, T, nh, hd = 64, 1024, 16, 64
+        ld = 3 * nh * hd
+        qkv = torch.randn(B * T, ld, device="cuda").bfloat16()
+        k, v = qkv[:, nh * hd:], qkv[:, 2 * nh * hd:]
+        o = torch.empty(B * T, nh * hd, device="cuda", dtype=torch.bfloat16)
+        lse = torch.empty(B, nh, T, device="cuda")
+        do = torch.randn(B * T, nh * hd, device="cuda").bfloat16()
+        dqkv = torch.empty_like(qkv)
+        ws = torch.empty(2, B, nh, T, device="cuda")
+
+        def fwd():
+            _ext.check(_ext.lib().nd_attn_fwd_ks(qkv.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
+                                                 B, nh, nh, T, hd, ld, nh * hd, 0, 0, hd ** -0.5, 0, _ext.stream_ptr()), "f")
+
+        def bwd():
+            _ext.check(_ext.lib().nd_attn_bwd_fused_ks(
+                qkv.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), dqkv.data_ptr(),
+                dqkv[:, nh * hd:].data_ptr(), dqkv[:, 2 * nh * hd:].data_ptr(), ws.data_ptr(), B, nh, nh, T, hd, ld,
+                nh * hd, 0, 0, hd ** -0.5, 0, 0, _ext.stream_ptr()), "b")
+        fwd()
+        out["attn_fwd"] = fwd
+        out["attn_bwd"] = bwd
     elif what == "epi":  # the fused-epilogue ping-pong GEMMs at the Llama-150M bench shapes
         from nanodiloco_amd.ops import gemm as G
         M, d, F = 65536, 1024, 2688
@@ -94,7 +117,7 @@ def workloads(what):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--alt", required=True)
-    ap.add_argument("--what", default="attn", choices=["attn", "step", "wgrad", "ce", "epi"])
+    ap.add_argument("--what", default="attn", choices=["attn", "attnk", "step", "wgrad", "ce", "epi"])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
