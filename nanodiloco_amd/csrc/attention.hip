@@ -329,7 +329,8 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
 // =============================================================================== forward
 // ABL (timing ablations only, wrong results; ND_ATTN_ABL): 1 no K/V DMA + no vmcnt wait, 2 no barrier,
 // 4 no softmax (P = bf16(S)), 8 no P V MFMAs, 16 no S MFMAs (S = 0 + lane constant).  Bit 32 is a
-// correct variant (cheaper mask, max tree, split row sum: needs T % 64 == 0).
+// correct variant (cheaper mask, max tree, split row sum: needs T % 64 == 0), the default of the
+// LDS-DMA path since the tile loop is unrolled (ND_ATTN_ABL=0 for the plain one).
 // NW: waves per workgroup (4 or 8; 8 = 256-query blocks, every K/V tile DMA'd once per 256 queries: DMA only)
 template <int HD, bool ROPE, bool DMA = false, bool PAD = false, int ABL = 0, int NW = 4>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
 __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA) ? 4 : 3)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
@@ -949,7 +950,7 @@ static int fwd_launch(const void* q, const void* k, const void* v, void* o, floa
                        (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr, attn_order());
   else if (T % 64 == 0 && fv != 'r') {
     const char* ae = getenv("ND_ATTN_ABL");
-    const int abl = ae ? atoi(ae) : 0;
+    const int abl = ae ? atoi(ae) : 32;  // default: the cheaper-mask / v_max3-tree variant (1.007-1.024x)
 #define ND_ABL(A)                                                                                                  \
   case A:                                                                                                          \
     hipLaunchKernelGGL((attn_fwd_kernel<HD, false, true, PAD, A>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, \
