@@ -776,26 +776,47 @@ __global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restri
     else wpp_vmn(more2 ? 4 : 0);        // A1(s + 1) landed
     wpp_bar();
   }
-  // epilogue: acc[a][b] lane l reg r = C[m0 + 128 g + 16 a + 4 (l >> 4) + r][n0 + 64 wn + 16 b + (l & 15)]
+  // epilogue: acc[a][b] lane l reg r = C[m0 + 128 g + 16 a + 4 (l >> 4) + r][n0 + 64 wn + 16 b + (l & 15)].
+  // Both groups first meet at the same barrier (group 1 ran one more), after which every LDS read and
+  // LDS-DMA write of the K-loop is done; each wave then transposes its 128 x 64 block through a private
+  // 16-KiB LDS region (two 64-row halves, 16-B chunk ^ (row & 15)) so the slab / C rows go out as
+  // 16-B-per-lane, 256-B-per-row stores instead of 4-B scalar ones.
+  if (g == 0) wpp_bar();  // group 1 ran one barrier more
   float* out = S == 1 ? C : slab + (int64_t)split * M * N;
   const int64_t ldo = S == 1 ? ldc : N;
+  float* reg = reinterpret_cast<float*>(smem) + w * (64 * 64);
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int half = 0; half < 2; ++half) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int n = n0 + wn * 64 + b * 16 + (lane & 15);
-      if (n >= N) continue;
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + g * 128 + a * 16 + 4 * (lane >> 4) + r;
-        if (m < M) {
-          float* p = out + (int64_t)m * ldo + n;
-          if (S == 1) *p += acc[a][b][r];
-          else *p = acc[a][b][r];
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * a + 4 * (lane >> 4) + r, col = 16 * b + (lane & 15);
+          reg[row * 64 + (((col >> 2) ^ (row & 15)) << 2) + (col & 3)] = acc[4 * half + a][b][r];
+        }
+    asm volatile("" ::: "memory");
+    const int c4 = lane & 15;
+    const int n = n0 + wn * 64 + 4 * c4;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = 4 * i + (lane >> 4);
+      const float4 v = *reinterpret_cast<const float4*>(reg + row * 64 + ((c4 ^ (row & 15)) << 2));
+      const int m = m0 + g * 128 + 64 * half + row;
+      if (m < M && n < N) {
+        float4* p = reinterpret_cast<float4*>(out + (int64_t)m * ldo + n);
+        if (S == 1) {
+          float4 c = *p;
+          c.x += v.x; c.y += v.y; c.z += v.z; c.w += v.w;
+          *p = c;
+        } else {
+          *p = v;
         }
       }
     }
-  if (g == 0) wpp_bar();  // group 1 ran one barrier more
+    asm volatile("" ::: "memory");
+  }
 }
 
 static int splits_for(int tiles, int K, int bk, int target) {
