@@ -268,14 +268,24 @@ __device__ __forceinline__ void store_T(bf16_t* out_row, f32x16* acc, float mul,
       }
     }
   }
+  // lanes l and l ^ 32 hold the two 4-wide halves of every 8-wide column group of one row: one
+  // v_permlane32_swap per word gives lane half 0 the whole group 2p and half 1 the whole group 2p + 1,
+  // so each lane writes 16-B chunks (NO x 2 stores) instead of 8-B ones (the epilogue store tail is
+  // issue-bound)
 #pragma unroll
   for (int o = 0; o < NO; ++o)
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d = o * 32 + 8 * g4 + 4 * h;
-      *reinterpret_cast<uint2*>(out_row + d) =
-          make_uint2(pack2(acc[o][4 * g4 + 0] * mul, acc[o][4 * g4 + 1] * mul),
-                     pack2(acc[o][4 * g4 + 2] * mul, acc[o][4 * g4 + 3] * mul));
+    for (int p = 0; p < 2; ++p) {
+      const int ga = 2 * p, gb = 2 * p + 1;
+      const uint32_t xa0 = pack2(acc[o][4 * ga + 0] * mul, acc[o][4 * ga + 1] * mul);
+      const uint32_t xa1 = pack2(acc[o][4 * ga + 2] * mul, acc[o][4 * ga + 3] * mul);
+      const uint32_t yb0 = pack2(acc[o][4 * gb + 0] * mul, acc[o][4 * gb + 1] * mul);
+      const uint32_t yb1 = pack2(acc[o][4 * gb + 2] * mul, acc[o][4 * gb + 3] * mul);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(xa0, yb0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(xa1, yb1, false, false);
+      // half 0: {own group-ga words, partner's group-ga words}; half 1: {partner's gb, own gb}
+      const int d = o * 32 + 8 * (h ? gb : ga);
+      *reinterpret_cast<uint4*>(out_row + d) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
     }
 }
 
