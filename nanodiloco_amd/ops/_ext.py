@@ -153,7 +153,7 @@ def _declare(L: ctypes.CDLL):
         # embedding
         "nd_embedding_fwd": [P, P, P, L64, I, I, P],
         "nd_embedding_bwd": [P, P, P, L64, I, I, P],
-        "nd_embedding_bwd_sorted": [P, P, P, P, L64, I, I, P],
+        "nd_embedding_bwd_sorted": [P, P, P, P, P, L64, I, I, P],
         # optimizer / outer step (flat buffers)
         "nd_sumsq_partial": [P, L64, P, I, P],
         "nd_adamw_step": [P, P, P, P, P, I, L64, P, I, F, F, F, F, F, F, F, F, P, I, P, P],

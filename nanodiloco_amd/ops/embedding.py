@@ -4,7 +4,9 @@ backward scatter-adds the residual gradient rows into the flat fp32 grad buffer.
 HIP path: ``nd_embedding_fwd`` (one wave per token row, 16-B vector loads) and
 ``nd_embedding_bwd`` (one wave per token row, f32 atomics on whole contiguous rows -- the
 access shape the MI355X atomic unit serves at full rate, MI355X_MICROARCH.md §Global float atomics),
-or, in deterministic mode (ops/determinism.py), ``nd_embedding_bwd_sorted`` over a stable argsort.
+or, in deterministic mode (ops/determinism.py), ``nd_embedding_bwd_sorted`` over a stable argsort
+(fixed 64-row chunks of the sorted order plus an ordered join of the runs that cross chunks, so a
+long run of one pad id does not serialise on one wave).
 """
 from __future__ import annotations
 
@@ -41,8 +43,9 @@ class EmbeddingFn(torch.autograd.Function):
                 if deterministic():
                     perm = torch.argsort(ids, stable=True)
                     sid = ids.index_select(0, perm).contiguous()
+                    ws = sorted_bwd_workspace(n, d, dy.device)
                     _ext.check(_ext.lib().nd_embedding_bwd_sorted(_ext.ptr(sid), _ext.ptr(perm), _ext.ptr(dy),
-                                                                  _ext.ptr(ctx.gw), n, d, ctx.vocab,
+                                                                  _ext.ptr(ctx.gw), _ext.ptr(ws), n, d, ctx.vocab,
                                                                   _ext.stream_ptr(dy.device)), "nd_embedding_bwd_sorted")
                 else:
                     _ext.check(_ext.lib().nd_embedding_bwd(_ext.ptr(ids), _ext.ptr(dy), _ext.ptr(ctx.gw), n, d,
@@ -57,6 +60,13 @@ class EmbeddingFn(torch.autograd.Function):
 
 
 _ANCHORS = {}
+
+SORTED_CHUNK = 64  # rows of the sorted order per wave in nd_embedding_bwd_sorted (kEmbChunk)
+
+
+def sorted_bwd_workspace(n, d, device):
+    """Head / tail partial sums of nd_embedding_bwd_sorted: 2 * ceil(n / 64) rows of d floats."""
+    return torch.empty(2 * ((n + SORTED_CHUNK - 1) // SORTED_CHUNK) * d, dtype=torch.float32, device=device)
 
 
 def _anchor(device):
