@@ -131,6 +131,8 @@ def wgrad_accumulate(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor):
 #   "blas" hipBLASLt through torch.mm -- the default: the own kernel reaches 0.94-1.01x of it per
 #          shape (profiles/r3_gemm_pp.md) and the step is 1.5 % faster this way
 #   "pp"   own ping-pong MFMA kernel (csrc/gemm_pp.hip; ops.gemm.gemm_pp) for every projection
+#   "short" own kernel for the short-K products (K <= 1024: o forward / dgrad, lm-head logits), where it
+#          is at parity per shape; hipBLASLt for the long-K dgrads (0.90x there)
 # The FUSED products always run on the own kernel (they exist only there): RoPE in the q|k|v
 # projection's epilogue, SwiGLU in the gate|up projection's, the SwiGLU backward in the down
 # projection's dgrad -- on by default (+0.8 % end to end over hipBLASLt + separate kernels,
@@ -139,7 +141,7 @@ _PROJ = {"gemm": "blas", "rope": True, "mlp": True}
 
 
 def set_proj_gemm(name: str) -> None:
-    if name not in ("pp", "blas"):
+    if name not in ("pp", "blas", "short"):
         raise ValueError(name)
     _PROJ["gemm"] = name
 
@@ -163,7 +165,7 @@ def fused_epilogues() -> dict:
 def _pp_ok(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, fused: bool = False) -> bool:
     """Shape / layout check for the own kernel; plain products also need the 'pp' selection (the
     fused-epilogue ops exist only on the own kernel and are switched by set_fused_epilogues)."""
-    if (_PROJ["gemm"] != "pp" and not fused) or not a.is_cuda:
+    if not a.is_cuda or not (fused or _PROJ["gemm"] == "pp" or (_PROJ["gemm"] == "short" and a.shape[-1] <= 1024)):
         return False
     from .gemm import pp_supported
     return pp_supported(a, b) and (out is None or (out.stride(-1) == 1 and out.stride(0) % 8 == 0
