@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--fp8-wgrad", action="store_true", help="with --fp8: weight-gradient GEMM in fp8 too")
     ap.add_argument("--fp8-gemm", default="hipblaslt", choices=["hip", "hipblaslt"],
                     help="with --fp8: forward / input-gradient fp8 GEMMs on our MFMA kernel or hipBLASLt")
+    ap.add_argument("--fp8-keep-fused", default="none", choices=["none", "rope", "mlp", "both"],
+                    help="with --fp8: projections that stay on the bf16 fused-epilogue GEMMs")
     ap.add_argument("--fp8-fused-quant", type=int, default=1, choices=[0, 1],
                     help="with --fp8: operand quantisation fused into the producing kernels (0: separate casts)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
@@ -100,6 +102,7 @@ def main():
         from nanodiloco_amd.ops import fp8 as _fp8
         _fp8.set_fused_quant(bool(a.fp8_fused_quant))
         _fp8.set_fp8_gemm(a.fp8_gemm)
+        _fp8.set_fp8_keep_fused(a.fp8_keep_fused)
     if a.wgrad_variant:
         os.environ["ND_WGRAD_VARIANT"] = a.wgrad_variant
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -111,7 +114,7 @@ def main():
         warmup_steps=100, total_steps=H * max(1, -(-10_000 // H)), inner_steps=H, lr=4e-4, outer_lr=0.7,
         llama_config_file=a.model, data="synthetic", ops=a.ops, backend=a.backend, inner_dp=a.inner_dp,
         comm_dtype=a.comm_dtype, bucket_mb=a.bucket_mb, overlap_outer=a.overlap_outer, fp8=a.fp8,
-        fp8_wgrad=a.fp8_wgrad, tuned_gemm=not a.no_tuned_gemm and not a.tuned_gemm_file,
+        fp8_wgrad=a.fp8_wgrad, fp8_keep_fused=a.fp8_keep_fused, tuned_gemm=not a.no_tuned_gemm and not a.tuned_gemm_file,
         hip_graph="on" if a.hip_graph else "off", wgrad_overlap=bool(a.wgrad_overlap), log_every=0, wandb="off",
         phase_timing=False, force_collectives=a.backend != "auto" and world == 1)
     tr = Trainer(targs)
@@ -233,6 +236,7 @@ def main():
             "proj_gemm": ops.proj_gemm(),
             "fused_epilogues": ops.fused_epilogues(),
             "fp8_gemm": a.fp8_gemm if a.fp8 else None,
+            "fp8_keep_fused": a.fp8_keep_fused if a.fp8 else None,
             "dgrad_transposed": ops.dgrad_transposed_enabled(),
             "ops": ops.get_backend() if a.ops != "auto" else ("hip" if env.device.type == "cuda" else "torch"),
         }

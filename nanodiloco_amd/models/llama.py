@@ -168,15 +168,21 @@ class LlamaForCausalLM:
                 ops.transpose_into(e[0], e[2])
                 e[1] = self.store.version
 
+    def _fp8_on(self, key: str) -> bool:
+        if self.fp8 is None:
+            return False
+        from ..ops.fp8 import fp8_projection
+        return fp8_projection(key.split(".")[1])
+
     def _linear(self, key, x, w, gw, x8=None):
-        if self.fp8 is not None:
+        if self._fp8_on(key):
             return self.fp8(key, x, w, gw, self.store.version, x8)
         return ops.linear(x, w, gw, self._wt(key, w))
 
     def _q8(self, key: str, grad: bool = False):
         """fp8 inner step: fused-producer quantisation target for projection ``key``'s input
         (``grad=False``) or output gradient (``grad=True``); None when not applicable."""
-        if self.fp8 is None or not self.training or not torch.is_grad_enabled():
+        if not self._fp8_on(key) or not self.training or not torch.is_grad_enabled():
             return None
         return self.fp8.dy_target(key) if grad else self.fp8.x_target(key)
 
@@ -188,8 +194,9 @@ class LlamaForCausalLM:
         qn = self._qkv_names[i]
         w_qkv = self._fused(qn, "shadow")
         rope_cols = (c.num_attention_heads + c.num_key_value_heads) * c.head_dim
-        wt_qkv = self._wt(f"{i}.qkv", w_qkv) if self.fp8 is None else None
-        if self.fp8 is None and ops.linear_rope_supported(y, w_qkv, wt_qkv, c.head_dim, rope_cols):
+        fp8_qkv = self._fp8_on(f"{i}.qkv")
+        wt_qkv = self._wt(f"{i}.qkv", w_qkv) if not fp8_qkv else None
+        if not fp8_qkv and ops.linear_rope_supported(y, w_qkv, wt_qkv, c.head_dim, rope_cols):
             # own GEMM with RoPE on q|k in its epilogue: the attention skips its rotation pass
             qkv = ops.linear_rope(y, w_qkv, self._fused(qn, "grad"), wt_qkv, cos, sin, T, c.head_dim, rope_cols)
             rotated = True
@@ -206,7 +213,7 @@ class LlamaForCausalLM:
         gn = self._gu_names[i]
         w_gu = self._fused(gn, "shadow")
         w_dn = self._w(p + "mlp.down_proj.weight")
-        if self.fp8 is None:
+        if not self._fp8_on(f"{i}.gu"):
             wt_gu, wt_dn = self._wt(f"{i}.gu", w_gu), self._wt(f"{i}.down", w_dn)
             if ops.mlp_fused_supported(y, w_gu, wt_gu, w_dn, wt_dn):
                 # own GEMMs with SwiGLU in the gate|up epilogue and its backward in the down dgrad's

@@ -62,6 +62,33 @@ def mm8(a8: torch.Tensor, b8: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) 
     return torch._scaled_mm(a8, b8.t(), sa, sb, out_dtype=torch.bfloat16)
 
 
+# Projections that stay on the bf16 fused-epilogue GEMMs under --fp8 (ops/linear.py): "rope" keeps
+# q|k|v + RoPE, "mlp" keeps gate|up + SwiGLU and the down dgrad + SwiGLU backward.  An fp8 GEMM
+# followed by the separate RoPE / SwiGLU pass can cost more than the fused bf16 GEMM it replaces.
+_KEEP = {"rope": False, "mlp": False}
+
+
+def set_fp8_keep_fused(mode: str) -> None:
+    """'none' (every decoder projection in fp8), 'rope', 'mlp' or 'both'."""
+    if mode not in ("none", "rope", "mlp", "both"):
+        raise ValueError(mode)
+    _KEEP["rope"] = mode in ("rope", "both")
+    _KEEP["mlp"] = mode in ("mlp", "both")
+
+
+def fp8_keep_fused() -> dict:
+    return dict(_KEEP)
+
+
+def fp8_projection(kind: str) -> bool:
+    """Whether decoder projection ``kind`` (qkv / o / gu / down) runs in fp8 under --fp8."""
+    if kind == "qkv":
+        return not _KEEP["rope"]
+    if kind in ("gu", "down"):
+        return not _KEEP["mlp"]
+    return True
+
+
 def set_fused_quant(enabled: bool) -> None:
     """Fused producer-side quantisation (default on) vs a separate cast per GEMM operand (A/B)."""
     _FUSED["enabled"] = bool(enabled)

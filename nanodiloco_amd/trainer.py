@@ -66,6 +66,8 @@ class TrainArgs:
     activation_checkpointing: bool = False
     fp8: bool = False              # fp8 e4m3/e5m2 decoder projections (GPU, bf16 compute)
     fp8_wgrad: bool = False        # with fp8: the weight-gradient GEMMs in fp8 too
+    fp8_keep_fused: str = "none"   # with fp8: none | rope | mlp | both -- projections kept on the bf16
+                                   # fused-epilogue GEMMs (ops/fp8.py set_fp8_keep_fused)
     force_collectives: bool = False  # world size 1: still create a (one-rank) process group and issue
                                      # every collective (exercises the RCCL path on one GPU)
     tuned_gemm: bool = True        # load the pre-tuned hipBLASLt algorithm table (ops/tuned_gemm.py)
@@ -166,6 +168,9 @@ class Trainer:
         self.grad_accum = a.batch_size // a.per_device_batch_size
         self.outer_steps = a.total_steps // a.inner_steps
         self.compute_dtype = _dtype(a.dtype, e.device)
+        if a.fp8 or a.dtype == "fp8":
+            from .ops.fp8 import set_fp8_keep_fused
+            set_fp8_keep_fused(a.fp8_keep_fused)
         self.model = LlamaForCausalLM(self.llama_config, e.device, self.compute_dtype,
                                       activation_checkpointing=a.activation_checkpointing,
                                       fp8=a.fp8 or a.dtype == "fp8", fp8_wgrad=a.fp8_wgrad).init_weights(a.seed)

@@ -123,6 +123,41 @@ def test_fp8_training_tracks_bf16(fp8_gemm):
     assert abs(f[-1] - b[-1]) < 0.15 * b[0], (b[-1], f[-1])
 
 
+@pytest.mark.parametrize("keep", ["rope", "mlp", "both"])
+def test_fp8_keep_fused_tracks_bf16(keep):
+    """--fp8-keep-fused: the kept projections run on the bf16 fused-epilogue GEMMs (no fp8 slot is
+    created for them), the rest in fp8; the model still trains like the bf16 one."""
+    cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=768, num_attention_heads=4,
+                                     num_key_value_heads=4, num_hidden_layers=2, vocab_size=512))
+    ids = torch.randint(0, 512, (8, 256), device="cuda")
+    losses = {}
+    try:
+        for mode in ("bf16", keep):
+            fp8.set_fp8_keep_fused("none" if mode == "bf16" else keep)
+            m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16, fp8=mode != "bf16").init_weights(5)
+            opt = FlatAdamW(m.store, lr=3e-3)
+            ls = []
+            for _ in range(30):
+                out = m(ids, labels=ids)
+                out.loss.backward()
+                opt.step()
+                if m.fp8 is not None:
+                    m.fp8.recipe.update()
+                m.store.zero_grad()
+                ls.append(out.loss.item())
+            losses[mode] = ls
+            if m.fp8 is not None:
+                kinds = {k.split(".")[1] for k in m.fp8.slots}
+                assert "o" in kinds
+                assert ("qkv" in kinds) == (keep == "mlp")
+                assert ("gu" in kinds) == ("down" in kinds) == (keep == "rope")
+    finally:
+        fp8.set_fp8_keep_fused("none")
+    b, f = losses["bf16"], losses[keep]
+    assert f[-1] < 0.5 * f[0], f
+    assert abs(f[-1] - b[-1]) < 0.15 * b[0], (b[-1], f[-1])
+
+
 # ----------------------------------------------------------------- fused producer-side quantisation
 def _target(fmt, scale=23.0):
     r = fp8.Fp8Recipe("cuda", capacity=4)
