@@ -49,3 +49,38 @@ def test_lm_head_ce_chunked_matches_unchunked():
     assert torch.allclose(l1, l2, atol=1e-5)
     assert torch.allclose(g1, g2, atol=1e-6)
     assert torch.allclose(gw1, gw2, atol=1e-5)
+
+
+def test_fp8_keep_fused_routing():
+    """--fp8-keep-fused: which decoder projections stay fp8 (measured default: all of them,
+    profiles/r3_fp8_keep_fused_ab.md)."""
+    assert fp8.fp8_keep_fused() == {"rope": False, "mlp": False}
+    want = {"none": {"qkv", "o", "gu", "down"}, "rope": {"o", "gu", "down"}, "mlp": {"qkv", "o"}, "both": {"o"}}
+    try:
+        for mode, kinds in want.items():
+            fp8.set_fp8_keep_fused(mode)
+            assert {k for k in ("qkv", "o", "gu", "down") if fp8.fp8_projection(k)} == kinds
+        with pytest.raises(ValueError):
+            fp8.set_fp8_keep_fused("all")
+    finally:
+        fp8.set_fp8_keep_fused("none")
+
+
+def test_proj_gemm_modes():
+    """Plain projection GEMM routing: hipBLASLt by default; 'short' / 'pp' select the own kernel
+    (never on CPU tensors); unknown names are rejected."""
+    import importlib
+
+    L = importlib.import_module("nanodiloco_amd.ops.linear")  # (ops.linear is the re-exported function)
+
+    assert L.proj_gemm() == "blas"
+    a, b = torch.randn(64, 128), torch.randn(32, 128)
+    try:
+        for mode in ("blas", "short", "pp"):
+            L.set_proj_gemm(mode)
+            assert not L._pp_ok(a, b)  # CPU tensors always take torch.mm
+            assert torch.allclose(L.mm_nt(a, b), a @ b.t())
+        with pytest.raises(ValueError):
+            L.set_proj_gemm("cublas")
+    finally:
+        L.set_proj_gemm("blas")
