@@ -102,9 +102,10 @@ def _dtype(name: str, device: torch.device) -> torch.dtype:
 
 
 # activation budget of one micro-batch as a share of device memory, and the micro-batch token target
-# (64 x 1024: the best of 16/32/64/128/256 sequences for Llama-150M on MI355X, docs/DESIGN.md §6)
+# (128 x 1024 at round-3 HEAD: +0.5 % bf16 / +1.8 % --fp8 over 64 x 1024 for Llama-150M in interleaved
+# A/Bs, profiles/r3_micro_batch_ab.md; Llama-1B is memory-capped at 64 x 1024, equal to 32 x 1024)
 _AUTO_MEM_SHARE = 0.3
-_AUTO_TOKENS = 65536
+_AUTO_TOKENS = 131072
 
 
 def auto_micro_batch(cfg: LlamaConfig, seq_len: int, batch_size: int, device: torch.device) -> int:
