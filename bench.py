@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--batch-size", type=int, default=256, help="sequences per worker per inner step (reference)")
     ap.add_argument("--micro-batch", default="auto",
                     help="sequences per forward/backward; auto = the trainer's --per-device-batch-size auto "
-                         "(64 for Llama-150M: best of 16/32/64/128/256 on MI355X, same global batch)")
+                         "(128 for Llama-150M: best of 16/32/64/128/256 on MI355X, same global batch; "
+                         "profiles/r3_micro_batch_ab.md)")
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--inner-steps", type=int, default=100)
     ap.add_argument("--inner-dp", type=int, default=1)

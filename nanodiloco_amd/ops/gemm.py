@@ -129,6 +129,24 @@ def gemm_pp_dswiglu(dy, w_down_t, gu, dgu_out=None):
     return dgu
 
 
+def gemm_w128(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """out[M, N] = a[M, K] . b[N, K]^T on the one-wave-per-SIMD kernel (csrc/gemm_w128.hip: 4 waves,
+    128 x 128 outputs per wave, one continuous MFMA stream per K-tile -- the hipBLASLt K-loop shape)."""
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_w128(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0), b.stride(0),
+                                       out.stride(0), _ext.stream_ptr(a.device)), "nd_gemm_w128")
+    return out
+
+
+def set_w128(group_m: int = -1, nt: int = -1) -> int:
+    """Tile grouping (m-panels per group) / non-temporal C stores of the w128 kernel (-1: unchanged);
+    returns the previous group size."""
+    return int(_ext.lib().nd_gemm_w128_set(int(group_m), int(nt)))
+
+
 def set_pp_variant(v: int) -> int:
     """Ablation builds of the ping-pong kernel (profiling only -- WRONG results): 1 no LDS-DMA in the
     loop, 2 no fragment reads, 3 both, 4 no barriers, 8 no epilogue stores, 15 all; 0 = the kernel."""

@@ -35,7 +35,7 @@ from .. import ops
 from ..models.llama import LlamaForCausalLM
 from ..optim import FlatAdamW, FlatOuterNesterov
 from ..utils.schedule import CosineWarmupSchedule
-from .comm import FlatCommunicator, plan_buckets
+from .comm import FlatCommunicator, PendingAllReduce, plan_buckets
 from .dist import DistEnv
 
 
@@ -257,6 +257,28 @@ class Diloco:
         """Apply a still-pending overlapped outer step (end of training / before checkpoint)."""
         if self._pending is not None:
             self._finish_outer()
+
+    def pending_outer_state(self) -> Optional[dict]:
+        """An overlapped outer step that is still in flight (a checkpoint between the boundary and its
+        one-step-late application): the compute stream waits for its all-reduce, and the reduced
+        pseudo-gradient plus this rank's drift base are returned WITHOUT applying the step, so a run
+        resumed from the checkpoint applies it at the same point as the uninterrupted run.  None when
+        nothing is pending (always, without ``overlap``)."""
+        if self._pending is None:
+            return None
+        self._pending[0].wait_all()
+        return {"delta": self.delta, "drift_base": self.drift_base}
+
+    def restore_pending_outer(self, delta: torch.Tensor, drift_base: torch.Tensor):
+        """Re-arm the pending outer step saved by :meth:`pending_outer_state` (its all-reduce already
+        done): the next :meth:`inner_step` applies it."""
+        if not self.overlap:
+            raise RuntimeError("checkpoint holds a pending overlapped outer step: resume with --overlap-outer")
+        self.delta.copy_(delta)
+        self.drift_base.copy_(drift_base)
+        ranges = plan_buckets(0, self.delta.numel(), self.delta.element_size(), self.outer_comm.bucket_bytes)
+        self._pending = (PendingAllReduce([None] * len(ranges), ranges, self.delta), self._sync_on_device(), None,
+                         time.perf_counter())
 
     # ------------------------------------------------------------------ debug
     @staticmethod

@@ -10,6 +10,8 @@ Here:
   ``force_pg=True`` creates a one-rank process group anyway (in-memory store, no rendezvous) and
   keeps every collective call live, so the RCCL path -- communicator init, bucketed async
   all-reduce, broadcast, sub-group all-gather, device barrier -- runs on a one-GPU box too;
+* RCCL groups use a high-priority HIP stream (``_pg_options``) so the side-stream collectives overlap
+  the compute stream instead of queueing behind it;
 * ``inner_dp = K`` splits the world into W/K DiLoCo workers of K GPUs each (BASELINE config 3).
   Inner groups are blocks of K consecutive ranks (xGMI neighbours on one node); outer groups are
   the ranks with the same index inside their inner group, so an outer all-reduce of shard r only
@@ -56,8 +58,35 @@ def _env_int(k, d):
     return int(v) if v not in (None, "") else d
 
 
+def _pg_options(backend: str, high_priority: bool):
+    """RCCL process groups run their collectives on a HIGH-PRIORITY HIP stream: the
+    bucketed outer all-reduce that ``--overlap-outer`` issues beside the next round's first inner step
+    (and the inner-DDP gradient buckets beside the backward) is then scheduled ahead of the compute
+    queue's kernels when both are ready."""
+    if backend != "nccl" or not high_priority:
+        return None
+    try:
+        from torch.distributed import ProcessGroupNCCL
+    except ImportError:  # torch built without RCCL
+        return None
+    return ProcessGroupNCCL.Options(is_high_priority_stream=True)
+
+
+def comm_stream_high_priority(group=None) -> Optional[bool]:
+    """Whether the RCCL backend of ``group`` (default: WORLD) was created with a high-priority stream
+    (None: no RCCL backend)."""
+    if not dist.is_initialized():
+        return None
+    g = group if group is not None else dist.group.WORLD
+    try:
+        be = g._get_backend(torch.device("cuda", torch.cuda.current_device()))
+        return bool(be.options.is_high_priority_stream)
+    except (RuntimeError, AttributeError):
+        return None
+
+
 def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[str] = None,
-                     timeout_s: float = 1800.0, force_pg: bool = False) -> DistEnv:
+                     timeout_s: float = 1800.0, force_pg: bool = False, high_priority: bool = True) -> DistEnv:
     rank = _env_int("RANK", 0)
     world = _env_int("WORLD_SIZE", 1)
     local_rank = _env_int("LOCAL_RANK", 0)
@@ -82,12 +111,17 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
     # silent hang) after `timeout_s`; torchrun --max-restarts + --resume then restart from the last
     # outer-step checkpoint.
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    pg_opts = _pg_options(backend, high_priority)
     if not dist.is_initialized():
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = dev  # eager RCCL communicator init
-        if world == 1 and "MASTER_ADDR" not in os.environ:
-            kw.update(store=dist.HashStore(), rank=0, world_size=1)  # one rank: nothing to rendezvous with
+            kw["pg_options"] = pg_opts
+        launched = "TORCHELASTIC_RUN_ID" in os.environ and "MASTER_PORT" in os.environ
+        if world == 1 and not launched:
+            # one rank outside torchrun: nothing to rendezvous with (a stray MASTER_ADDR without
+            # MASTER_PORT / RANK must not send us into an env:// rendezvous)
+            kw.update(store=dist.HashStore(), rank=0, world_size=1)
         dist.init_process_group(**kw)
     env.backend = backend
     env.force_collectives = world == 1
@@ -98,13 +132,13 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
     else:
         for w in range(env.num_workers):  # every rank must create every group, in the same order
             ranks = list(range(w * inner_dp, (w + 1) * inner_dp))
-            g = dist.new_group(ranks)
+            g = dist.new_group(ranks, pg_options=pg_opts)
             if w == env.worker:
                 env.inner_group = g
         if env.num_workers > 1:
             for r in range(inner_dp):
                 ranks = list(range(r, world, inner_dp))
-                g = dist.new_group(ranks)
+                g = dist.new_group(ranks, pg_options=pg_opts)
                 if r == env.inner_rank:
                     env.outer_group = g
     return env

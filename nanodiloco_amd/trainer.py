@@ -110,7 +110,7 @@ _AUTO_TOKENS = 131072
 
 def auto_micro_batch(cfg: LlamaConfig, seq_len: int, batch_size: int, device: torch.device) -> int:
     """``--per-device-batch-size auto``: the largest divisor of ``batch_size`` whose micro-batch holds at
-    most ~64k tokens and whose activations (flash attention, no recompute: ~34 * d bytes per token and
+    most ``_AUTO_TOKENS`` = 128k tokens (128 x 1024 for Llama-150M) and whose activations (flash attention, no recompute: ~34 * d bytes per token and
     layer in bf16, plus the chunked lm-head's 4 GiB logits budget) fit in 30 % of the device memory.
 
     The math does not change: gradients are the mean over the micro-batches of an inner step (each
@@ -210,13 +210,16 @@ class Trainer:
         if hg == "auto":
             # HF batches always carry an attention_mask, which the captured graph does not take:
             # never capture (and hold the graph's memory) for a data source that produces masks
+            # a forced one-rank process group arms the inner-DDP communicator (async RCCL all-reduces with
+            # host-side pending events), which a captured graph would replay with stale events
             use_graph = (e.device.type == "cuda" and e.inner_dp == 1 and self.model.fp8 is None
-                         and self.data_kind != "hf" and self.llama_config.num_params() < 100_000_000)
+                         and self.data_kind != "hf" and not a.force_collectives
+                         and self.llama_config.num_params() < 100_000_000)
         else:
             use_graph = hg in ("1", "true", "on", "yes")
         if use_graph:
-            if e.device.type != "cuda" or e.inner_dp > 1 or self.model.fp8 is not None:
-                raise ValueError("--hip-graph needs a GPU, --inner-dp 1 and no --fp8")
+            if e.device.type != "cuda" or e.inner_dp > 1 or self.model.fp8 is not None or a.force_collectives:
+                raise ValueError("--hip-graph needs a GPU, --inner-dp 1, no --fp8 and no --force-collectives")
             from .utils.graphs import GraphedMicroStep
             self.graphed = GraphedMicroStep(self.model)
         self.run_name = create_run_name("nanodiloco", self.run_config, is_debug=False)

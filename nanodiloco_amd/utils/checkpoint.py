@@ -6,7 +6,13 @@ Directory layout (written only at outer-step boundaries, when all replicas are i
   <dir>/model.safetensors        fp32 master weights, HF key names -> ``LlamaForCausalLM.from_pretrained(dir)``
   <dir>/diloco_state.safetensors outer state shared by all workers: theta_sync, outer momentum
   <dir>/rank{r}.safetensors      per-rank inner AdamW m/v + data-generator state
-  <dir>/trainer_state.json       step counters, schedule, hyper-params, per-rank scalar state
+  <dir>/trainer_state.json       step counters, schedule, hyper-params, topology (world size, inner_dp,
+                                 flat size -- validated on resume), per-rank scalar state
+
+With ``--overlap-outer`` a checkpoint taken at an outer boundary holds that step still PENDING (its
+all-reduce finished, its one-step-late application not yet done): the reduced pseudo-gradient and each
+rank's drift base and local weights go into the rank files, and the resumed run applies the step after its first inner
+step -- the same trajectory as the uninterrupted run (tests/test_e2e_cpu.py).
 
 Only safetensors + JSON: nothing executable is ever deserialised.
 """
@@ -36,7 +42,7 @@ def _load_st(path: str) -> Dict[str, torch.Tensor]:
 
 def save_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, step: int, data_state: Optional[Dict[str, Any]] = None,
                     extra: Optional[Dict[str, Any]] = None):
-    diloco.finalize()
+    pending = diloco.pending_outer_state()  # overlapped mode: saved as pending, not applied
     if env.inner_dp > 1:
         # two-level mode: each GPU of a worker updates only its shard of the outer momentum
         # (parallel/diloco.py, sharded outer step); gather the worker's full buffer before rank 0
@@ -48,6 +54,12 @@ def save_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, step: int, data_
     # per-rank state (every rank)
     per = {"adamw.exp_avg": diloco.inner_optimizer.exp_avg, "adamw.exp_avg_sq": diloco.inner_optimizer.exp_avg_sq}
     scal: Dict[str, Any] = {"adamw_step": diloco.inner_optimizer.step_count}
+    if pending is not None:
+        # until the pending step lands, every worker's local weights differ (each carries its own
+        # inner progress since the boundary): model.safetensors holds rank 0's, each rank keeps its own
+        per["outer.delta"] = pending["delta"]
+        per["outer.drift_base"] = pending["drift_base"]
+        per["master"] = store.master
     if data_state:
         for k, v in data_state.items():
             if isinstance(v, torch.Tensor):
@@ -67,7 +79,7 @@ def save_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, step: int, data_
         state = {"step": step, "local_step": diloco.local_step, "outer_step_count": diloco.outer_step_count,
                  "outer_opt_step": diloco.outer_optimizer.step_count, "scheduler": diloco.scheduler.state_dict(),
                  "world_size": env.world_size, "inner_dp": env.inner_dp, "flat_numel": store.numel,
-                 **(extra or {})}
+                 "pending_outer": pending is not None, **(extra or {})}
         with open(os.path.join(ckpt_dir, "trainer_state.json"), "w") as f:
             json.dump(state, f, indent=2)
     barrier(env)
@@ -77,6 +89,13 @@ def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv) -> Dict[str, Any
     with open(os.path.join(ckpt_dir, "trainer_state.json")) as f:
         state = json.load(f)
     store = model.store
+    # topology: every rank restores its OWN AdamW state and (two-level mode) its shard of the outer
+    # step, so a resume on a different layout would silently drop workers' state or mis-shard the
+    # outer momentum -- refuse it
+    for key, have in (("world_size", env.world_size), ("inner_dp", env.inner_dp), ("flat_numel", store.numel)):
+        if key in state and int(state[key]) != int(have):
+            raise ValueError(f"checkpoint {ckpt_dir} was written with {key}={state[key]}, this run has {have}: "
+                             f"resume needs the same world size, --inner-dp and model")
     sd = _load_st(os.path.join(ckpt_dir, "model.safetensors"))
     model.load_state_dict(sd)
     ds = _load_st(os.path.join(ckpt_dir, "diloco_state.safetensors"))
@@ -86,8 +105,14 @@ def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv) -> Dict[str, Any
                             "outer_step_count": state["outer_step_count"]})
     rfile = os.path.join(ckpt_dir, f"rank{env.rank}.safetensors")
     data_state: Dict[str, Any] = {}
+    if not os.path.exists(rfile) and "world_size" in state:
+        raise FileNotFoundError(f"{rfile} missing: the checkpoint is incomplete for rank {env.rank}")
     if os.path.exists(rfile):
         per = _load_st(rfile)
+        if state.get("pending_outer"):
+            store.master.copy_(per["master"].to(store.master.device))
+            diloco.restore_pending_outer(per["outer.delta"].to(diloco.delta.device),
+                                         per["outer.drift_base"].to(diloco.delta.device))
         diloco.inner_optimizer.exp_avg.copy_(per["adamw.exp_avg"])
         diloco.inner_optimizer.exp_avg_sq.copy_(per["adamw.exp_avg_sq"])
         with open(os.path.join(ckpt_dir, f"rank{env.rank}.json")) as f:

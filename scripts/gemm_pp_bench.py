@@ -54,11 +54,12 @@ def check():
                       (16384, 3072, 1024), (32768, 2688, 256), (9000, 1000, 320)]:
         a, b = r(m, k), r(n, k) * 0.05
         ref = a.float() @ b.float().t()
-        y = G.gemm_pp(a, b)
-        e = rel(y, ref, f"{m}x{n}x{k}")
-        ok = e < 1e-2
-        bad += not ok
-        print(f"check gemm_pp {m}x{n}x{k}: rel {e:.2e} {'ok' if ok else 'FAIL'}", flush=True)
+        for nm, fn in (("gemm_pp", G.gemm_pp), ("gemm_w128", G.gemm_w128)):
+            y = fn(a, b)
+            e = rel(y, ref, f"{nm} {m}x{n}x{k}")
+            ok = e < 1e-2
+            bad += not ok
+            print(f"check {nm} {m}x{n}x{k}: rel {e:.2e} {'ok' if ok else 'FAIL'}", flush=True)
     # strided operands / output (views into wider buffers)
     a_w, b_w, o_w = r(512, 1024), r(384, 768) * 0.05, torch.zeros(512, 520, device="cuda", dtype=torch.bfloat16)
     a, b, o = a_w[:, :640], b_w[:, :640], o_w[:, :384]
@@ -166,7 +167,8 @@ def main():
     def plain(name, m, n, k):
         x, w = r(m, k), r(n, k) * 0.05
         out = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
-        arms = {"blas": lambda: torch.mm(x, w.t(), out=out), "pp": lambda: G.gemm_pp(x, w, out)}
+        arms = {"blas": lambda: torch.mm(x, w.t(), out=out), "pp": lambda: G.gemm_pp(x, w, out),
+                "w128": lambda: G.gemm_w128(x, w, out)}
         cases.append((name, 2.0 * m * n * k, arms))
 
     plain("qkv fwd", M, qkv_n, d)

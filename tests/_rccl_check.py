@@ -89,6 +89,10 @@ def main():
     check(dist.is_initialized() and dist.get_backend() == BACKEND and env.backend == BACKEND,
           f"one-rank {BACKEND} group")
     check(env.force_collectives and env.is_distributed, "collectives forced on at world size 1")
+    if not CPU:
+        from nanodiloco_amd.parallel.dist import comm_stream_high_priority
+        hp = comm_stream_high_priority()
+        check(hp is True, f"RCCL collectives on a high-priority stream (got {hp})")
 
     # ---- bucketed async all-reduce, per-bucket waits on the compute stream
     comm = FlatCommunicator(None, 1, bucket_mb=1.0, force=True)

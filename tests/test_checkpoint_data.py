@@ -52,6 +52,47 @@ def test_checkpoint_roundtrip_and_resume(tmp_path):
     assert d.outer_step_count == d2.outer_step_count == 2
 
 
+def test_checkpoint_refuses_other_topology(tmp_path):
+    """A resume with another world size / --inner-dp / model would drop workers' AdamW state or
+    mis-shard the outer momentum: load_checkpoint refuses it."""
+    m, d = _mk()
+    save_checkpoint(str(tmp_path), m, d, DistEnv(), step=0)
+    st = json.load(open(tmp_path / "trainer_state.json"))
+    assert (st["world_size"], st["inner_dp"], st["flat_numel"], st["pending_outer"]) == (1, 1, m.store.numel, False)
+    for key, val in (("world_size", 2), ("inner_dp", 2), ("flat_numel", m.store.numel + 64)):
+        bad = dict(st, **{key: val})
+        json.dump(bad, open(tmp_path / "trainer_state.json", "w"))
+        m2, d2 = _mk(1)
+        with pytest.raises(ValueError, match=key):
+            load_checkpoint(str(tmp_path), m2, d2, DistEnv())
+    json.dump(st, open(tmp_path / "trainer_state.json", "w"))
+    os.remove(tmp_path / "rank0.safetensors")
+    with pytest.raises(FileNotFoundError):
+        load_checkpoint(str(tmp_path), *_mk(1), DistEnv())
+
+
+def test_checkpoint_keeps_overlapped_outer_step_pending(tmp_path):
+    """--overlap-outer: a checkpoint at the boundary saves the outer step as pending; resumed, the
+    next inner step applies it -- same weights as the run that never stopped."""
+    def mk(seed):
+        m = LlamaForCausalLM(LlamaConfig.from_dict(CFG)).init_weights(seed)
+        return m, Diloco(m, FlatAdamW(m.store, lr=1e-3), FlatOuterNesterov(m.store), 2, 8, 4, env=DistEnv(),
+                         overlap=True)
+    m, d = mk(0)
+    _train(m, d, 4, torch.Generator().manual_seed(0))
+    assert d._pending is not None
+    save_checkpoint(str(tmp_path), m, d, DistEnv(), step=4)
+    assert json.load(open(tmp_path / "trainer_state.json"))["pending_outer"] is True
+    assert d._pending is not None  # saving did not apply it
+    _train(m, d, 4, torch.Generator().manual_seed(1))
+    m2, d2 = mk(99)
+    load_checkpoint(str(tmp_path), m2, d2, DistEnv())
+    assert d2._pending is not None
+    _train(m2, d2, 4, torch.Generator().manual_seed(1))
+    d.finalize(), d2.finalize()
+    assert torch.equal(m.store.master, m2.store.master) and torch.equal(d.sync, d2.sync)
+
+
 def test_checkpoint_loads_into_hf(tmp_path):
     transformers = pytest.importorskip("transformers")
     m, d = _mk(3)

@@ -60,13 +60,17 @@ def _tensors(path):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("nproc,inner_dp", [(2, 1), (4, 2)])
-def test_resume_matches_uninterrupted(tmp_path, nproc, inner_dp):
+@pytest.mark.parametrize("nproc,inner_dp,overlap", [(2, 1, False), (4, 2, False), (2, 1, True)])
+def test_resume_matches_uninterrupted(tmp_path, nproc, inner_dp, overlap):
     """Stop after 2 outer steps, resume, finish: bit-identical to the uninterrupted run -- weights,
-    theta_sync and (two-level mode) every shard of the outer momentum."""
+    theta_sync and (two-level mode) every shard of the outer momentum.  With --overlap-outer the
+    checkpoint holds the boundary's outer step still pending and the resumed run applies it one inner
+    step late, exactly like the uninterrupted run (checkpointing does not change the trajectory)."""
     a, b = tmp_path / "a", tmp_path / "b"
     la, lb = tmp_path / "a.jsonl", tmp_path / "b.jsonl"
     common = BASE + ["--inner-steps", "2", "--data", "synthetic", "--inner-dp", str(inner_dp)]
+    if overlap:
+        common += ["--overlap-outer"]
     _torchrun(nproc, common + ["--total-steps", "6", "--checkpoint-dir", str(a), "--log-file", str(la)], tmp_path)
     # interrupted run: 4 steps + checkpoint every outer step, then resume to 6
     _torchrun(nproc, common + ["--total-steps", "6", "--stop-at-step", "4", "--checkpoint-dir", str(b),
@@ -75,6 +79,8 @@ def test_resume_matches_uninterrupted(tmp_path, nproc, inner_dp):
                                "--checkpoint-dir", str(b)], tmp_path)
     ra, rb = _log(la), _log(lb)
     assert [x["step"] for x in rb] == [5, 6]
+    if overlap:
+        assert json.load(open(b / "trainer_state.json"))["pending_outer"] is False  # final save: applied
     assert ra[-1]["loss"] == rb[-1]["loss"]
     for f in ("model.safetensors", "diloco_state.safetensors"):
         ta, tb = _tensors(a / f), _tensors(b / f)
