@@ -73,7 +73,7 @@ def parse():
                     help="attention backward: row statistics inside the dQ kernel (0: separate passes)")
     ap.add_argument("--dgrad-t", type=int, default=1, choices=[0, 1],
                     help="input-gradient GEMMs on transposed weight copies (K-contiguous NT layout)")
-    ap.add_argument("--proj-gemm", default="blas", choices=["pp", "blas", "short"],
+    ap.add_argument("--proj-gemm", default="blas", choices=["pp", "blas", "short", "w128"],
                     help="plain projection / lm-head GEMMs: hipBLASLt (blas, default) or the own ping-pong "
                          "MFMA kernel (pp); the fused-epilogue GEMMs always run on the own kernel")
     ap.add_argument("--fused-rope", type=int, default=1, choices=[0, 1],

@@ -63,7 +63,11 @@ def _run(cmd):
 
 # Per-file extra flags.  attention.hip: no SLP vectorisation -- packed f32 VALU (v_pk_mul_f32 /
 # v_pk_fma_f32) issued beside MFMAs costs more than two scalar ops (MI355X_MICROARCH price list).
-FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"],
+              # gemm_w128.hip: its phases are 64-slot loops that must unroll completely (every
+              # accumulator index a constant); past the default pragma threshold the accumulator array
+              # silently moves to scratch
+              "gemm_w128.hip": ["-mllvm", "-pragma-unroll-threshold=1000000"]}
 
 
 def build(force: bool = False, jobs: int = 0, save_temps: bool = False, verbose: bool = False) -> dict:
@@ -75,6 +79,16 @@ def build(force: bool = False, jobs: int = 0, save_temps: bool = False, verbose:
     flags += shlex.split(os.environ.get("ND_EXTRA_HIPCC_FLAGS", ""))  # A/B or ablation builds only
     if save_temps:
         flags += ["-save-temps"]
+    kern = os.path.join(LIB_DIR, "libnd_kernels.so")
+    # fast path: the library was linked from exactly these sources / headers / flags (object files do
+    # not travel to the GPU box, so without this every fresh checkout would recompile everything)
+    src_key = " ".join(flags) + repr(sorted(FILE_FLAGS.items()))
+    src_stamp = kern + ".src.sha256"
+    all_src = sources + sorted(headers)
+    if not force and os.path.exists(kern) and os.path.exists(src_stamp):
+        with open(src_stamp) as f:
+            if f.read().strip() == _digest(all_src, src_key):
+                return _build_runtime(force, kern, [])
     todo = []
     objs = []
     for s in sources:
@@ -104,11 +118,16 @@ def build(force: bool = False, jobs: int = 0, save_temps: bool = False, verbose:
         for s in ex.map(comp, todo):
             if verbose:
                 print(f"[build] compiled {os.path.basename(s)}", flush=True)
-    kern = os.path.join(LIB_DIR, "libnd_kernels.so")
     if force or todo or _stale(objs, kern):
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", kern + ".tmp"] + objs)
         os.replace(kern + ".tmp", kern)
         _mark(objs, kern)
+    with open(src_stamp, "w") as f:
+        f.write(_digest(all_src, src_key))
+    return _build_runtime(force, kern, todo)
+
+
+def _build_runtime(force, kern, todo) -> dict:
     # host runtime (plain C++)
     rt_src = sorted(glob.glob(os.path.join(HERE, "runtime", "*.cpp")))
     rt = os.path.join(LIB_DIR, "libnd_runtime.so")

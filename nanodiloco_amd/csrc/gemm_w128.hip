@@ -5,35 +5,33 @@
 // TensileLibrary_BB_BB_HA_Bias_SAV_..._gfx950.co) is NOT a ping-pong pair: 4 waves, ONE wave per SIMD,
 // 128 x 128 outputs per wave (8 x 8 v_mfma_f32_16x16x32_bf16 accumulators = all 256 AGPRs), and a
 // single continuous MFMA stream of 128 MFMAs per 64-deep K-tile into which that same wave weaves its
-// 32 ds_read_b128 fragment reads, its 16 LDS-DMA pieces and three barriers.  Per SIMD that is 32
-// fragment reads per K-tile instead of the ping-pong pair's 48 (128 x 128 per wave reuses every
-// fragment 8 times instead of 4 / 8), and the matrix pipe never waits for a partner's phase.
+// 32 ds_read_b128 fragment reads, its 16 LDS-DMA pieces (8 rows x 128 B: whole cache lines) and its
+// barriers.  Per SIMD that is 32 fragment reads per K-tile instead of the ping-pong pair's 48.
 //
 // This kernel is that structure, written for our layouts and epilogues:
 //
 //   * 256 threads; wave w: rows 128 (w >> 1) .., columns 128 (w & 1) .. of the 256 x 256 tile.
-//   * Each K-tile is two PHASES of 64 MFMAs (k-step 0 = k 0..31, k-step 1 = k 32..63).  LDS holds two
-//     K-tile buffers, each split by k-HALF ([h][A 256 rows x 64 B | B 256 rows x 64 B], 16-B chunk
-//     index XOR-swizzled by swz4(row >> 2) on the DMA source address and on the reads -- conflict-free
-//     for the ds_read_b128 lane groups).  Stream position i (tile, K-tile) lives in buffer i & 1:
+//   * LDS: two K-tile buffers of [A 256 rows x 128 B | B 256 rows x 128 B], 16-B chunk index XOR
+//     (row >> 1) & 7 (on the DMA source address -- LDS-DMA writes lane-linear -- and on the reads).
+//     Every DMA piece is 8 whole 128-B rows: a k-split into 64-B half rows measured 30 % slower (twice
+//     the cache-line requests per byte; session r4c ablations, profiles/r4_gemm_w128.md).
+//   * Each K-tile i (buffer i & 1) is two PHASES of 64 MFMAs:
 //
-//       phase 1 of i:  MFMAs on F0 (k-half 0 of i, in registers)
-//                      reads  F1 <- k-half 1 of i            DMA  k-half 0 of i + 2 -> buffer i & 1
-//                      then   lgkmcnt(0), vmcnt(16): k-half 0 of i + 1 has landed
-//       phase 2 of i:  MFMAs on F1
-//                      reads  F0 <- k-half 0 of i + 1        DMA  k-half 1 of i + 2 -> buffer i & 1
-//                      then   lgkmcnt(0), vmcnt(16): k-half 1 of i + 1 has landed
+//       phase 1:  MFMAs on F0 (k-step 0 of i, in registers)
+//                 reads F1 <- A k-step 1 of i, lgkmcnt(0), BARRIER (A half of buffer i & 1 free),
+//                 reads F1 <- B k-step 1 of i, DMA A of tile i + 2 -> buffer i & 1
+//                 then lgkmcnt(0), vmcnt(8): all of tile i + 1 has landed
+//       phase 2:  BARRIER (B half free; tile i + 1 visible), MFMAs on F1
+//                 DMA B of tile i + 2 -> buffer i & 1 (first half), reads F0 <- k-step 0 of i + 1
 //
-//     ONE barrier per phase, issued after the phase's first two MFMAs (they need only registers), so
-//     each DMA has two phases (~2k cycles) to land and every wait is a counted vmcnt.  WAR: a k-half
-//     is restaged only after the barrier that follows the lgkmcnt(0) retiring its last reads.
+//     Two barriers per K-tile, each placed between MFMAs; the only vmcnt wait leaves the next
+//     tile's A pieces in flight.  A DMA piece has 2-2.5 phases to land.
 //   * Persistent grid (one workgroup per CU, XCD-remapped tile walk with GM m-panel groups, as
-//     gemm_pp).  A tile's epilogue runs inside the next tile's first phase: the 16-row block a of the
-//     finished accumulators is converted and stored right before the new tile's zero-input MFMAs
-//     overwrite acc[a][*], so its VALU / store issue overlaps the MFMA pipe.
-//   * The B fragment rows are permuted (block 2p + e, lane row i -> B row 32 p + 8 (i >> 2) + 4 e +
-//     (i & 3)) so that each lane's accumulators of blocks 2p, 2p + 1 are 8 CONSECUTIVE output columns:
-//     one 16-B store per (row block, block pair) with no cross-lane shuffle.
+//     gemm_pp).  OVL: a tile's epilogue is woven into its last phase (row block a - 1 stored 5 MFMAs
+//     after its last one), else it runs between the tiles.
+//   * B rows are stored PERMUTED in LDS (DMA source rows; reads stay natural) so that each lane's
+//     accumulators of column blocks 2p, 2p + 1 are 8 CONSECUTIVE output columns: one 16-B store per
+//     (row block, block pair), no cross-lane shuffle.
 //
 // Reference role: every nn.Linear of HF LlamaForCausalLM (/root/reference/nanodiloco/main.py:97-99,
 // run at :109-111).
@@ -46,14 +44,10 @@ using namespace nd;
 namespace {
 typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
 constexpr int TM = 256, TN = 256, TK = 64;
-constexpr uint32_t OPH = 256 * 64;  // one operand's k-half: 256 rows x 64 B (16 KiB)
-constexpr uint32_t KH = 2 * OPH;    // A + B of one k-half (32 KiB)
-constexpr uint32_t BUFB = 2 * KH;   // one K-tile buffer (64 KiB)
-constexpr int LGKM0 = 0xC07F;       // s_waitcnt lgkmcnt(0), vmcnt / expcnt at their maxima
+constexpr uint32_t BUFB0 = 2 * 256 * 128;  // one K-tile buffer (A + B, 64 KiB) without padding
+constexpr int LGKM0 = 0xC07F;        // s_waitcnt lgkmcnt(0), vmcnt / expcnt at their maxima
 
 enum : int { W_STORE = 0 };
-
-__device__ __forceinline__ int swz4(int r) { return (0x1320 >> (4 * (r & 3))) & 3; }  // 0, 2, 3, 1
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
@@ -65,6 +59,11 @@ __device__ __forceinline__ void dma(__amdgpu_buffer_rsrc_t r, uint32_t voff, uin
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds) : "memory");
 }
+// m0 set one MFMA ahead of its piece (nothing else in these kernels reads m0), then the bare load
+__device__ __forceinline__ void set_m0(uint32_t lds) { asm volatile("s_mov_b32 m0, %0" ::"s"(lds) : "memory"); }
+__device__ __forceinline__ void dma_go(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r) : "memory");
+}
 __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -73,11 +72,14 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 template <int N> __device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+template <int ABL, int N> __device__ __forceinline__ void vmwait_l() {
+  if constexpr ((ABL & 16) == 0) vmwait<N>();
+}
 // MFMAs as inline asm on accumulators pinned to AGPRs with a TIED operand ("+a"): the zero-input
 // form of a tile's first k-step then overwrites exactly the registers the previous tile's epilogue has
 // just read (a free "=a" result lets the register allocator park the whole old tile in VGPRs and
 // spill).  The compiler sees no MFMA, so the code that reads an accumulator after its last MFMA
-// waits for the result itself (drain()).
+// waits for the result itself (drain(), or 5 MFMAs in between).
 __device__ __forceinline__ void mma(const bf16x8& a, const bf16x8& b, f32x4& c) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
@@ -88,18 +90,39 @@ __device__ __forceinline__ void drain() { asm volatile("s_nop 15\n\ts_nop 3" :::
 
 // stores per wave per tile (8 row blocks x 4 column pairs)
 constexpr int NST = 32;
+// phase slots of the A DMA pieces (phase 1, after the A barrier) and of the B pieces (phase 2)
+// (every covered read is retired 8+ MFMAs after its issue: an lgkmcnt right behind a read stalls the
+// lone wave for the read's latency)
+__host__ __device__ constexpr bool a_rd1_slot(int s) { return s >= 1 && s <= 15 && (s - 1) % 2 == 0; }   // A k-step 1
+constexpr int A_BAR = 23;                                                                             // A free
+__host__ __device__ constexpr bool a_dma_slot(int s) { return s >= 24 && (s - 24) % 5 == 0 && s <= 59; }
+__host__ __device__ constexpr bool b_rd1_slot(int s) { return s >= 26 && s <= 47 && (s - 26) % 3 == 0; }  // B k-step 1
+// phase 2: the B pieces early (they have the rest of this phase and the next one to land)
+__host__ __device__ constexpr bool b_dma_slot(int s) { return s >= 3 && s <= 31 && (s - 3) % 4 == 0; }
+constexpr int B_DMA_LAST = 31;
+// epilogue stores issued after the last B piece of a LAST phase (epi(a - 1) at slot 8 a + 4, epi(7) after)
+__host__ __device__ constexpr int nst_tail() {
+  int n = 4;
+  for (int a = 1; a < 8; ++a) n += (8 * a + 4 > B_DMA_LAST) ? 4 : 0;
+  return n;
+}
 
-template <int EPI, int STP>
+// ABL: ablation builds for profiling only (WRONG results): 1 no LDS-DMA in the phases, 2 no fragment
+// reads in the phases, 4 no barriers in the phases, 8 no epilogue stores, 16 no vmcnt waits in the loop
+template <int EPI, int STP, bool OVL, int ABL = 0>
 __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                            bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
                                                            int64_t ldb, int64_t ldc, int GM) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // LDS layout: 32-row blocks (4 KiB: one DMA piece per wave) at a stride PS (hipBLASLt's 64-B pad
+  // per block measured +-0: r4_gemm_w128.md)
+  constexpr uint32_t PS = 4096u;
+  constexpr uint32_t OPB = 8 * PS, BUFB = 2 * OPB;
   const int tn = (N + TN - 1) / TN, tmn = (M + TM - 1) / TM, tiles = tmn * tn;
   const int G = gridDim.x;  // <= tiles (host)
   const int first = xcd_remap(blockIdx.x, G);
   const int my_tiles = (tiles - 1 - first) / G + 1;
   const int nk = K / TK;
-  const int total = my_tiles * nk;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = w >> 1, wn = w & 1;
@@ -117,15 +140,18 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
     }
   };
 
-  // ---- LDS-DMA: piece j (0..3) of an operand's k-half = 16-row block w + 4 j; lane -> row l >> 2,
-  // physical chunk l & 3 (lane-linear), which holds logical chunk (l & 3) ^ swz4(row >> 2)
-  uint32_t voa[4], vob[4];
+  // ---- LDS-DMA: piece j (0..7) of an operand = LDS rows 8 (w + 4 j) .. + 7 (1 KiB); lane -> LDS row
+  // l >> 3, physical chunk l & 7 (lane-linear), which holds logical chunk (l & 7) ^ ((row >> 1) & 7).
+  // A: LDS row = tile row.  B: LDS row j holds tile column g(j) (the permutation above).
+  uint32_t voa[8], vob[8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = 16 * (w + 4 * j) + (lane >> 2);
-    const int lch = (lane & 3) ^ swz4(lane >> 4);
+  for (int j = 0; j < 8; ++j) {
+    const int row = 8 * (w + 4 * j) + (lane >> 3);
+    const int lch = (lane & 7) ^ ((row >> 1) & 7);
+    const int jj = row & 127, blk = jj >> 4, i = jj & 15;
+    const int gcol = (row & 128) + 32 * (blk >> 1) + 8 * (i >> 2) + 4 * (blk & 1) + (i & 3);
     voa[j] = (uint32_t)(((int64_t)row * lda + lch * 8) * 2);
-    vob[j] = (uint32_t)(((int64_t)row * ldb + lch * 8) * 2);
+    vob[j] = (uint32_t)(((int64_t)gcol * ldb + lch * 8) * 2);
   }
   struct Pos { int lt, kt, m0, n0; };
   auto pos_init = [&](Pos& p, int s) __attribute__((always_inline)) {
@@ -140,50 +166,50 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
       if (p.lt < my_tiles) coords(first + p.lt * G, p.m0, p.n0);
     }
   };
-  // descriptors of k-half h of stream position p (zero records past the stream's end: the pieces
-  // are still issued -- constant vmcnt counts -- but read nothing)
-  auto rs_a = [&](const Pos& p, int h) __attribute__((always_inline)) {
-    const int64_t e0 = (int64_t)p.m0 * lda + (int64_t)p.kt * TK + h * 32;
+  // descriptors of K-tile p (zero records past the stream's end: the pieces are still issued --
+  // constant vmcnt counts -- but read nothing)
+  auto rs_a = [&](const Pos& p) __attribute__((always_inline)) {
+    const int64_t e0 = (int64_t)p.m0 * lda + (int64_t)p.kt * TK;
     const int64_t lim = (int64_t)M * lda - e0;
     const bool ok = p.lt < my_tiles && lim > 0;
     return rsrc(A + (ok ? e0 : 0), ok ? (uint32_t)(lim < 0x3fffffff ? lim * 2 : 0x7ffffffe) : 0u);
   };
-  auto rs_b = [&](const Pos& p, int h) __attribute__((always_inline)) {
-    const int64_t e0 = (int64_t)p.n0 * ldb + (int64_t)p.kt * TK + h * 32;
+  auto rs_b = [&](const Pos& p) __attribute__((always_inline)) {
+    const int64_t e0 = (int64_t)p.n0 * ldb + (int64_t)p.kt * TK;
     const int64_t lim = (int64_t)N * ldb - e0;
     const bool ok = p.lt < my_tiles && lim > 0;
     return rsrc(B + (ok ? e0 : 0), ok ? (uint32_t)(lim < 0x3fffffff ? lim * 2 : 0x7ffffffe) : 0u);
   };
-  auto stage_all = [&](const Pos& p, int s, int h) __attribute__((always_inline)) {
-    const uint32_t d = lds0 + (uint32_t)(s & 1) * BUFB + (uint32_t)h * KH + (uint32_t)w * 1024u;
-    const auto ra = rs_a(p, h), rb = rs_b(p, h);
+  auto stage_all = [&](const Pos& p, int s) __attribute__((always_inline)) {
+    const uint32_t d = lds0 + (uint32_t)(s & 1) * BUFB + (uint32_t)w * 1024u;
+    const auto ra = rs_a(p), rb = rs_b(p);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dma(ra, voa[j], d + (uint32_t)j * 4096u);
+    for (int j = 0; j < 8; ++j) dma(ra, voa[j], d + (uint32_t)j * PS);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dma(rb, vob[j], d + OPH + (uint32_t)j * 4096u);
+    for (int j = 0; j < 8; ++j) dma(rb, vob[j], d + OPB + (uint32_t)j * PS);
   };
 
-  // ---- fragment reads (per-lane byte offsets inside one k-half): A block a = rows 128 wm + 16 a + r16,
-  // B block 2 p + e = rows 128 wn + 32 p + 8 (r16 >> 2) + 4 e + (r16 & 3); chunk q ^ swz4(row >> 2)
+  // ---- fragment reads: A block a = LDS rows 128 wm + 16 a + r16, B block b = LDS rows 128 wn + 16 b + r16;
+  // k-step ks: logical chunk 4 ks + q, physical ^ ((row >> 1) & 7) = ^ ((r16 >> 1) & 7)
   const int r16 = lane & 15, q = lane >> 4;
-  const uint32_t fa_off = (uint32_t)((128 * wm + r16) * 64 + ((q ^ swz4(r16 >> 2)) << 4));
-  uint32_t fb_off[2];
+  uint32_t fa_off[2], fb_off[2];
 #pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int row = 128 * wn + 8 * (r16 >> 2) + 4 * e + (r16 & 3);
-    fb_off[e] = OPH + (uint32_t)(row * 64 + ((q ^ swz4(row >> 2)) << 4));
+  for (int ks = 0; ks < 2; ++ks) {
+    const uint32_t o = (uint32_t)(r16 * 128 + (((4 * ks + q) ^ ((r16 >> 1) & 7)) << 4));
+    fa_off[ks] = o + (uint32_t)wm * 4u * PS;
+    fb_off[ks] = o + OPB + (uint32_t)wn * 4u * PS;
   }
-  auto rd = [&](uint32_t base, int r, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) __attribute__((always_inline)) {
-    if (r < 8) {
-      fa[r] = *reinterpret_cast<const bf16x8*>(smem + base + fa_off + r * 1024);
-    } else {
-      const int b = r - 8;
-      fb[b] = *reinterpret_cast<const bf16x8*>(smem + base + fb_off[b & 1] + (b >> 1) * 2048);
-    }
+  // 16-row block a: 32-row block a >> 1, half a & 1
+  auto rd_a = [&](uint32_t base, int ks, int a, bf16x8 (&fa)[8]) __attribute__((always_inline)) {
+    fa[a] = *reinterpret_cast<const bf16x8*>(smem + base + fa_off[ks] + (a >> 1) * PS + (a & 1) * 2048);
+  };
+  auto rd_b = [&](uint32_t base, int ks, int b, bf16x8 (&fb)[8]) __attribute__((always_inline)) {
+    fb[b] = *reinterpret_cast<const bf16x8*>(smem + base + fb_off[ks] + (b >> 1) * PS + (b & 1) * 2048);
   };
 
   f32x4 acc[8][8];
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  int pm0 = 0, pn0 = 0;  // tile of the accumulators (for its epilogue)
 
   // ---- epilogue of the 16-row block a of the tile (m0, n0): lane row r16, columns 8 q + 0..7 of each
   // 32-column block pair -> one 16-B store per pair; rows past M drop through the descriptor, columns
@@ -194,96 +220,144 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
     const int lrow = 128 * wm + 16 * a + r16;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      // the accumulators reach VGPRs HERE (an empty asm with a VGPR operand tied to the AGPR value):
+      // the accumulators reach VGPRs HERE, one v_accvgpr_read per element from an AGPR operand:
       // left to itself the register allocator hoists all 256 AGPR reads to the epilogue's start
       f32x4 x, y;
-      asm volatile("" : "=v"(x) : "0"(acc[a][2 * p]));
-      asm volatile("" : "=v"(y) : "0"(acc[a][2 * p + 1]));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(x[r]) : "a"(acc[a][2 * p][r]));
+        asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(y[r]) : "a"(acc[a][2 * p + 1][r]));
+      }
       const u32x4 d = u32x4{pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(y[0], y[1]), pack2(y[2], y[3])};
       const int col = n0 + 128 * wn + 32 * p + 8 * q;
       const uint32_t off = col < N ? (uint32_t)(((int64_t)lrow * ldc + col) * 2) : 0x80000000u;
-      __builtin_amdgcn_raw_buffer_store_b128(d, cr, off, 0, STP);
+      if constexpr ((ABL & 8) != 0) asm volatile("" ::"v"(d), "v"(off));
+      else __builtin_amdgcn_raw_buffer_store_b128(d, cr, off, 0, STP);
     }
   };
 
-  // ---- one phase: 64 MFMAs (row block a = s >> 3, column block b = s & 7) with the phase's 16
-  // fragment reads and 8 DMA pieces woven in; the barrier after slot 1.  FIRST: zero-input MFMAs;
-  // FAT: the previous tile's epilogue of row block a right before slot 8 a
-  auto phase = [&](auto FIRST, auto FAT, bf16x8 (&ua)[8], bf16x8 (&ub)[8], uint32_t rbase, bf16x8 (&ra_)[8],
-                   bf16x8 (&rb_)[8], __amdgpu_buffer_rsrc_t dra, __amdgpu_buffer_rsrc_t drb, uint32_t dlds, int pm0,
-                   int pn0) __attribute__((always_inline)) {
-    constexpr bool F = decltype(FIRST)::value, FT = decltype(FAT)::value;
+  // ---- phase 1 of K-tile (buffer cur): 64 MFMAs on F0; F1 <- k-step 1 of cur (A reads, barrier, B
+  // reads); DMA A of tile i + 2 into cur after the barrier.  hook: the scalar work for phase 2
+  // (descriptors, coordinates) between the MFMAs
+  auto phase1 = [&](auto FIRST, uint32_t cur, __amdgpu_buffer_rsrc_t dra, uint32_t dlds, auto&& hook)
+      __attribute__((always_inline)) {
+    constexpr bool F = decltype(FIRST)::value;
 #pragma unroll
     for (int s = 0; s < 64; ++s) {
       const int a = s >> 3, b = s & 7;
-      if constexpr (FT) {
-        if (b == 0) {
-          epi(a, pm0, pn0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
+      if constexpr (F) mma0(fb0[b], fa0[a], acc[a][b]);
+      else mma(fb0[b], fa0[a], acc[a][b]);
+      if (!(ABL & 2)) {
+        if (a_rd1_slot(s)) rd_a(cur, 1, (s - 1) / 2, fa1);
+        if (b_rd1_slot(s)) rd_b(cur, 1, (s - 26) / 3, fb1);
       }
-      if constexpr (F) mma0(ub[b], ua[a], acc[a][b]);
-      else mma(ub[b], ua[a], acc[a][b]);
-      if (s == 1) bar();
-      if (s >= 2 && s <= 47 && (s - 2) % 3 == 0) rd(rbase, (s - 2) / 3, ra_, rb_);
-      if (s >= 3 && (s - 3) % 8 == 0) {
-        const int j = (s - 3) / 8;
-        if (j < 4) dma(dra, voa[j], dlds + (uint32_t)j * 4096u);
-        else dma(drb, vob[j - 4], dlds + OPH + (uint32_t)(j - 4) * 4096u);
+      if (s == A_BAR) {  // every wave's A k-step-1 reads retired -> the A half of cur is free
+        __builtin_amdgcn_s_waitcnt(LGKM0);
+        if (!(ABL & 4)) bar();
       }
+      if (a_dma_slot(s) && !(ABL & 1)) dma_go(dra, voa[(s - 24) / 5]);
+      // m0 for the next slot's piece, one MFMA ahead (the bare load then issues without a wait state)
+      if (a_dma_slot(s + 1) && !(ABL & 1)) set_m0(dlds + (uint32_t)((s + 1 - 24) / 5) * PS);
+      if (s == 40) hook();
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  // ---- phase 2: barrier (the B half of cur free; tile i + 1 landed and visible); 64 MFMAs on F1;
+  // F0 <- k-step 0 of tile i + 1 (buffer nxt); DMA B of tile i + 2 into cur.  LAST: the tile's epilogue
+  // woven in (row block a - 1 five MFMAs after its last one)
+  auto phase2 = [&](auto LAST, uint32_t nxt, __amdgpu_buffer_rsrc_t drb, uint32_t dlds, auto&& hook)
+      __attribute__((always_inline)) {
+    constexpr bool L = decltype(LAST)::value;
+#pragma unroll
+    for (int s = 0; s < 64; ++s) {
+      const int a = s >> 3, b = s & 7;
+      mma(fb1[b], fa1[a], acc[a][b]);
+      if (s == 1 && !(ABL & 4)) bar();
+      if (!(ABL & 2) && s >= 2 && s <= 47 && (s - 2) % 3 == 0) {
+        const int r = (s - 2) / 3;
+        if (r < 8) rd_a(nxt, 0, r, fa0);
+        else rd_b(nxt, 0, r - 8, fb0);
+      }
+      if (b_dma_slot(s) && !(ABL & 1)) dma_go(drb, vob[(s - 3) / 4]);
+      if (b_dma_slot(s + 1) && !(ABL & 1)) set_m0(dlds + OPB + (uint32_t)((s + 1 - 3) / 4) * PS);
+      if (s == 30) hook();
+      if constexpr (L) {
+        if (b == 4 && a > 0) epi(a - 1, pm0, pn0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (L) {
+      drain();
+      epi(7, pm0, pn0);
+    }
+  };
 
-  // ---- prologue: stream positions 0 and 1 staged, position 0 landed, its k-half 0 in F0
+  // ---- prologue: tiles 0 and 1 staged, tile 0 landed, its k-step 0 in F0
   {
     Pos p;
     pos_init(p, 0);
-    stage_all(p, 0, 0);
-    stage_all(p, 0, 1);
+    stage_all(p, 0);
     pos_init(p, 1);
-    stage_all(p, 1, 0);
-    stage_all(p, 1, 1);
+    stage_all(p, 1);
   }
   vmwait<16>();
   bar();
 #pragma unroll
-  for (int r = 0; r < 16; ++r) rd(0, r, fa0, fb0);
+  for (int a = 0; a < 8; ++a) rd_a(0, 0, a, fa0);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) rd_b(0, 0, b, fb0);
   __builtin_amdgcn_s_waitcnt(LGKM0);
 
-  Pos p2;  // stream position i + 2: the DMA target of iteration i
+  Pos p2;  // K-tile i + 2: the DMA target of iteration i
   pos_init(p2, 2);
-  int pm0 = 0, pn0 = 0;  // tile of the accumulators (epilogue of the FAT phase)
-
-  auto iteration = [&](auto FIRST, auto FAT, int i) __attribute__((always_inline)) {
-    constexpr bool FT = decltype(FAT)::value;
+  __amdgpu_buffer_rsrc_t dA = rs_a(p2);
+  constexpr int NST_TAIL = nst_tail();
+  // FIRST: the tile's first K-tile (zero-input MFMAs); LAST: its last, with the epilogue woven into its
+  // second phase (OVL).  after_epi: 1 the previous iteration was a LAST one, 2 the between-tile
+  // epilogue preceded -- its stores are younger than the pieces the phase-1 wait retires
+  auto iteration = [&](auto FIRST, auto LAST, int i, int after_epi) __attribute__((always_inline)) {
     const uint32_t cur = (uint32_t)(i & 1) * BUFB, nxt = (uint32_t)((i + 1) & 1) * BUFB;
     const uint32_t dlds = lds0 + cur + (uint32_t)w * 1024u;
-    int em0 = pm0, en0 = pn0;
-    if constexpr (decltype(FIRST)::value) {  // this tile's coordinates, for the next epilogue
-      const int lt = i / nk;
-      coords(first + lt * G, pm0, pn0);
-    }
-    // phase 1: F0; reads F1 <- k-half 1 of i; DMA k-half 0 of i + 2
-    phase(FIRST, FAT, fa0, fb0, cur + KH, fa1, fb1, rs_a(p2, 0), rs_b(p2, 0), dlds, em0, en0);
+    __amdgpu_buffer_rsrc_t dB;
+    phase1(FIRST, cur, dA, dlds, [&]() __attribute__((always_inline)) {
+      dB = rs_b(p2);
+      if constexpr (decltype(FIRST)::value) coords(first + (i / nk) * G, pm0, pn0);  // this tile's epilogue
+    });
     __builtin_amdgcn_s_waitcnt(LGKM0);
-    vmwait<FT ? 16 + NST : 16>();
-    // phase 2: F1; reads F0 <- k-half 0 of i + 1; DMA k-half 1 of i + 2
-    phase(std::false_type{}, std::false_type{}, fa1, fb1, nxt, fa0, fb0, rs_a(p2, 1), rs_b(p2, 1), dlds + KH, 0, 0);
+    // tile i + 1 landed: its A pieces came in iteration i - 1's phase 1, its B pieces in its phase 2;
+    // younger: this phase's A pieces of tile i + 2, and any epilogue stores after i + 1's last B piece
+    if (after_epi == 1) vmwait_l<ABL, 8 + NST_TAIL>();
+    else if (after_epi == 2) vmwait_l<ABL, 8 + NST>();
+    else vmwait_l<ABL, 8>();
+    phase2(LAST, nxt, dB, dlds, [&]() __attribute__((always_inline)) {
+      pos_next(p2);
+      dA = rs_a(p2);
+    });
     __builtin_amdgcn_s_waitcnt(LGKM0);
-    vmwait<FT ? 16 + NST : 16>();
-    pos_next(p2);
   };
-
-  for (int lt = 0, i = 0; lt < my_tiles; ++lt) {
-    iteration(std::true_type{}, std::false_type{}, i++);
-    for (int kt = 1; kt < nk; ++kt) iteration(std::false_type{}, std::false_type{}, i++);
-    // the tile's epilogue (v1: between the tiles, matrix pipe idle; the next tile's DMA is in flight)
+  auto epilogue_all = [&]() __attribute__((always_inline)) {
     drain();
 #pragma unroll
     for (int a = 0; a < 8; ++a) {
       epi(a, pm0, pn0);
       __builtin_amdgcn_sched_barrier(0);  // one row block at a time: bounded epilogue registers
+    }
+  };
+  const std::false_type NO;
+  const std::true_type YES;
+  if constexpr (OVL) {
+    // nk >= 2 (host): every tile = FIRST, plain K-tiles, LAST with the epilogue inside its second phase
+    for (int lt = 0, i = 0; lt < my_tiles; ++lt) {
+      iteration(YES, NO, i++, lt > 0 ? 1 : 0);
+      for (int kt = 1; kt < nk - 1; ++kt) iteration(NO, NO, i++, 0);
+      iteration(NO, YES, i++, 0);
+    }
+  } else {
+    for (int lt = 0, i = 0; lt < my_tiles; ++lt) {
+      iteration(YES, NO, i++, lt > 0 ? 2 : 0);
+      for (int kt = 1; kt < nk; ++kt) iteration(NO, NO, i++, 0);
+      // the tile's epilogue between the tiles (matrix pipe idle; the next tile's DMA is in flight)
+      epilogue_all();
     }
   }
   vmwait<0>();  // trailing zero-record DMA pieces: retired before the workgroup's LDS is released
@@ -303,20 +377,45 @@ int num_cus_w128() {
   return n;
 }
 
-int g_w128_nt = 1;  // non-temporal C stores
+int g_w128_nt = 1;   // non-temporal C stores
+int g_w128_ovl = 1;  // epilogue woven into each tile's last phase (0: between the tiles)
+int g_w128_abl = 0;  // ablation builds (profiling only, wrong results): nd_gemm_w128_set_ablation
 
-template <int EPI, int STP>
+template <int EPI, int STP, bool OVL, int ABL = 0>
 int launch_w128_v(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
                   hipStream_t s) {
-  const size_t lds = 2 * (size_t)BUFB;  // 128 KiB
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_w128_kernel<EPI, STP>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const size_t lds = 2 * (size_t)BUFB0;  // 128 KiB
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&gemm_w128_kernel<EPI, STP, OVL, ABL>), hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)lds);
   if (attr != hipSuccess) return (int)attr;
   const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   const int grid = tiles < num_cus_w128() ? tiles : num_cus_w128();
-  hipLaunchKernelGGL((gemm_w128_kernel<EPI, STP>), dim3(grid), dim3(256), lds, s, (const bf16_t*)A, (const bf16_t*)B,
-                     (bf16_t*)C, M, N, K, lda, ldb, ldc, g_w128_group_m);
+  hipLaunchKernelGGL((gemm_w128_kernel<EPI, STP, OVL, ABL>), dim3(grid), dim3(256), lds, s, (const bf16_t*)A,
+                     (const bf16_t*)B, (bf16_t*)C, M, N, K, lda, ldb, ldc, g_w128_group_m);
   ND_LAUNCH_CHECK();
+}
+
+template <int EPI>
+int launch_w128(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
+                hipStream_t s) {
+  if constexpr (EPI == W_STORE) {
+    switch (g_w128_abl) {
+      case 1: return launch_w128_v<EPI, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, s);
+      case 2: return launch_w128_v<EPI, 2, false, 2>(A, B, C, M, N, K, lda, ldb, ldc, s);
+      case 3: return launch_w128_v<EPI, 2, false, 3>(A, B, C, M, N, K, lda, ldb, ldc, s);
+      case 4: return launch_w128_v<EPI, 2, false, 4>(A, B, C, M, N, K, lda, ldb, ldc, s);
+      case 8: return launch_w128_v<EPI, 2, false, 8>(A, B, C, M, N, K, lda, ldb, ldc, s);
+      case 16: return launch_w128_v<EPI, 2, false, 16>(A, B, C, M, N, K, lda, ldb, ldc, s);
+      case 31: return launch_w128_v<EPI, 2, false, 31>(A, B, C, M, N, K, lda, ldb, ldc, s);
+      default: break;
+    }
+  }
+  if (g_w128_ovl && K >= 2 * TK)
+    return g_w128_nt ? launch_w128_v<EPI, 2, true>(A, B, C, M, N, K, lda, ldb, ldc, s)
+                     : launch_w128_v<EPI, 0, true>(A, B, C, M, N, K, lda, ldb, ldc, s);
+  return g_w128_nt ? launch_w128_v<EPI, 2, false>(A, B, C, M, N, K, lda, ldb, ldc, s)
+                   : launch_w128_v<EPI, 0, false>(A, B, C, M, N, K, lda, ldb, ldc, s);
 }
 
 bool w128_shapes_ok(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
@@ -331,13 +430,19 @@ bool w128_shapes_ok(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) 
 ND_API int nd_gemm_w128(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb,
                         int64_t ldc, hipStream_t s) {
   if (!w128_shapes_ok(M, N, K, lda, ldb, ldc)) return (int)hipErrorInvalidValue;
-  return g_w128_nt ? launch_w128_v<W_STORE, 2>(A, B, C, M, N, K, lda, ldb, ldc, s)
-                   : launch_w128_v<W_STORE, 0>(A, B, C, M, N, K, lda, ldb, ldc, s);
+  return launch_w128<W_STORE>(A, B, C, M, N, K, lda, ldb, ldc, s);
 }
 
-ND_API int nd_gemm_w128_set(int group_m, int nt) {
+ND_API int nd_gemm_w128_set_ablation(int v) {
+  const int old = g_w128_abl;
+  g_w128_abl = v;
+  return old;
+}
+
+ND_API int nd_gemm_w128_set(int group_m, int nt, int ovl) {
   const int old = g_w128_group_m;
   if (group_m >= 0) g_w128_group_m = group_m;
   if (nt >= 0) g_w128_nt = nt;
+  if (ovl >= 0) g_w128_ovl = ovl;
   return old;
 }

@@ -176,7 +176,8 @@ def _declare(L: ctypes.CDLL):
         "nd_gemm_pp_set_variant": [I],
         # one-wave-per-SIMD projection GEMM (csrc/gemm_w128.hip)
         "nd_gemm_w128": [P, P, P, I, I, I, L64, L64, L64, P],
-        "nd_gemm_w128_set": [I, I],
+        "nd_gemm_w128_set": [I, I, I],
+        "nd_gemm_w128_set_ablation": [I],
         # weight-gradient GEMM
         "nd_wgrad_splits": [I, I, I],
         "nd_wgrad": [P, P, P, P, I, I, I, L64, L64, L64, P],

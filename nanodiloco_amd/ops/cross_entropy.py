@@ -4,7 +4,8 @@ The reference materialises fp32 logits ``[N, V]`` and their gradient (1.05 GB ea
 micro-batch; 33.5 GB at 262k tokens).  Here the N rows are processed in
 chunks; for each chunk:
 
-  1. ``logits = y_c @ W^T``            (own GEMM, csrc/gemm_pp.hip; compute dtype)
+  1. ``logits = y_c @ W^T``            (the plain projection GEMM, ops.linear.mm_nt: the selected
+                                       --proj-gemm kernel; compute dtype)
   2. ``nd_ce_fwd_bwd``                 one HIP kernel, one row per workgroup: online max/sum-exp over V,
                                        per-row loss summed into a device scalar, and the logits
                                        buffer overwritten IN PLACE by ``dlogits = (softmax - onehot) * s``

@@ -141,10 +141,10 @@ def gemm_w128(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> tor
     return out
 
 
-def set_w128(group_m: int = -1, nt: int = -1) -> int:
-    """Tile grouping (m-panels per group) / non-temporal C stores of the w128 kernel (-1: unchanged);
-    returns the previous group size."""
-    return int(_ext.lib().nd_gemm_w128_set(int(group_m), int(nt)))
+def set_w128(group_m: int = -1, nt: int = -1, ovl: int = -1) -> int:
+    """Tile grouping (m-panels per group) / non-temporal C stores / epilogue overlapped with the next
+    tile's first phase, of the w128 kernel (-1: unchanged); returns the previous group size."""
+    return int(_ext.lib().nd_gemm_w128_set(int(group_m), int(nt), int(ovl)))
 
 
 def set_pp_variant(v: int) -> int:
@@ -186,3 +186,9 @@ def wgrad(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
     ws = _workspace(gw.device, S * M * N) if S > 1 else None
     _ext.check(L.nd_wgrad(_ext.ptr(dy), _ext.ptr(x), _ext.ptr(gw), _ext.ptr(ws), M, N, K, dy.stride(0), x.stride(0),
                           gw.stride(0), _ext.stream_ptr(gw.device)), "nd_wgrad")
+
+
+def set_w128_ablation(v: int) -> int:
+    """Ablation builds of the w128 kernel (profiling only -- WRONG results): 1 no LDS-DMA, 2 no fragment
+    reads, 4 no barriers, 8 no epilogue stores, 16 no vmcnt waits in the loop, 31 all; 0 = the kernel."""
+    return int(_ext.lib().nd_gemm_w128_set_ablation(int(v)))

@@ -133,6 +133,9 @@ def wgrad_accumulate(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor):
 #   "pp"   own ping-pong MFMA kernel (csrc/gemm_pp.hip; ops.gemm.gemm_pp) for every projection
 #   "short" own kernel for the short-K products (K <= 1024: o forward / dgrad, lm-head logits), where it
 #          is at parity per shape; hipBLASLt for the long-K dgrads (0.90x there)
+#   "w128" own one-wave-per-SIMD kernel (csrc/gemm_w128.hip: hipBLASLt's K-loop shape, 128 x 128 per
+#          wave): 0.93-0.95x hipBLASLt per shape (profiles/r4_gemm_w128.md), ahead of "pp" on the long-K
+#          products (lm-head dgrad 0.91x vs 0.87x)
 # The FUSED products always run on the own kernel (they exist only there): RoPE in the q|k|v
 # projection's epilogue, SwiGLU in the gate|up projection's, the SwiGLU backward in the down
 # projection's dgrad -- on by default (+0.8 % end to end over hipBLASLt + separate kernels,
@@ -141,7 +144,7 @@ _PROJ = {"gemm": "blas", "rope": True, "mlp": True}
 
 
 def set_proj_gemm(name: str) -> None:
-    if name not in ("pp", "blas", "short"):
+    if name not in ("pp", "blas", "short", "w128"):
         raise ValueError(name)
     _PROJ["gemm"] = name
 
@@ -165,7 +168,7 @@ def fused_epilogues() -> dict:
 def _pp_ok(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, fused: bool = False) -> bool:
     """Shape / layout check for the own kernel; plain products also need the 'pp' selection (the
     fused-epilogue ops exist only on the own kernel and are switched by set_fused_epilogues)."""
-    if not a.is_cuda or not (fused or _PROJ["gemm"] == "pp" or (_PROJ["gemm"] == "short" and a.shape[-1] <= 1024)):
+    if not a.is_cuda or not (fused or _PROJ["gemm"] in ("pp", "w128") or (_PROJ["gemm"] == "short" and a.shape[-1] <= 1024)):
         return False
     from .gemm import pp_supported
     return pp_supported(a, b) and (out is None or (out.stride(-1) == 1 and out.stride(0) % 8 == 0
@@ -176,8 +179,8 @@ def mm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> torch.T
     """a[M, K] . b[N, K]^T on the selected projection GEMM (the own kernel when 'pp' is selected and
     it takes the shape; hipBLASLt otherwise)."""
     if _pp_ok(a, b, out):
-        from .gemm import gemm_pp
-        return gemm_pp(a, b, out)
+        from .gemm import gemm_pp, gemm_w128
+        return gemm_w128(a, b, out) if _PROJ["gemm"] == "w128" else gemm_pp(a, b, out)
     library_gemm_fence(a.device if a.is_cuda else None)
     return torch.mm(a, b.t(), out=out) if out is not None else torch.mm(a, b.t())
 

@@ -21,7 +21,7 @@ def load(path):
     calls = collections.defaultdict(set)
     seen = set()
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "")[:44]
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")[:44]
         agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
         key = (r["Dispatch_Id"], r["Process_Id"])
         calls[name].add(key)

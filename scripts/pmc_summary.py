@@ -19,7 +19,7 @@ def main(path, top=12):
     calls = collections.defaultdict(set)
     seen = set()
     for r in rows:
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "")[:48]
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")[:48]
         agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
         key = (r["Dispatch_Id"], r["Process_Id"])
         calls[name].add(key)

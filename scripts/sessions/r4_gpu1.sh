@@ -3,7 +3,7 @@
 # against hipBLASLt and the ping-pong kernel at 131,072 tokens
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r4a
+O=gpurun_out/${SESSION:-r4a}
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 400 python -u -m pytest tests/test_gemm_w128_gpu.py -x -q --timeout 120 --timeout-method thread > $O/test.log 2>&1

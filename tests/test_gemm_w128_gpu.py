@@ -11,15 +11,18 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True, params=[4, 1, 3], ids=lambda g: f"gm{g}")
+@pytest.fixture(autouse=True, params=[(4, 0), (1, 0), (3, 1), (4, 1)], ids=lambda p: f"gm{p[0]}-ovl{p[1]}")
 def _hip(hip_lib, request):
+    """Tile orders (grouped by 4 m-panels, row-major, a grouping with a short last group) x the two
+    epilogue placements (between the tiles / inside each tile's last phase)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ops.set_backend("hip")
-    old = G.set_w128(group_m=request.param)
+    gm, ovl = request.param
+    old = G.set_w128(group_m=gm, ovl=ovl)
     torch.manual_seed(0)
     yield
-    G.set_w128(group_m=old)
+    G.set_w128(group_m=old, ovl=0)
     ops.set_backend("auto")
 
 
