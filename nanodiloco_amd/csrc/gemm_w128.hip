@@ -64,6 +64,10 @@ __device__ __forceinline__ void set_m0(uint32_t lds) { asm volatile("s_mov_b32 m
 __device__ __forceinline__ void dma_go(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
   asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r) : "memory");
 }
+// FLAT-global form of the piece (saddr + 32-bit voffset, no range check): ABL 4096 probe only
+__device__ __forceinline__ void gdma_go(const void* sbase, uint32_t voff) {
+  asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase) : "memory");
+}
 __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -108,7 +112,8 @@ __host__ __device__ constexpr int nst_tail() {
 }
 
 // ABL: ablation builds for profiling only (WRONG results): 1 no LDS-DMA in the phases, 2 no fragment
-// reads in the phases, 4 no barriers in the phases, 8 no epilogue stores, 16 no vmcnt waits in the loop
+// reads in the phases, 4 no barriers in the phases, 8 no epilogue stores, 16 no vmcnt waits in the loop;
+// 4096: the loop's pieces as FLAT-global LDS loads (no range check: exact-multiple shapes only)
 template <int EPI, int STP, bool OVL, int ABL = 0>
 __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                            bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
@@ -239,6 +244,8 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
   // ---- phase 1 of K-tile (buffer cur): 64 MFMAs on F0; F1 <- k-step 1 of cur (A reads, barrier, B
   // reads); DMA A of tile i + 2 into cur after the barrier.  hook: the scalar work for phase 2
   // (descriptors, coordinates) between the MFMAs
+  const bf16_t* gpa = A;  // ABL 4096 probe: FLAT-global piece base pointers of K-tile i + 2
+  const bf16_t* gpb = B;
   auto phase1 = [&](auto FIRST, uint32_t cur, __amdgpu_buffer_rsrc_t dra, uint32_t dlds, auto&& hook)
       __attribute__((always_inline)) {
     constexpr bool F = decltype(FIRST)::value;
@@ -255,7 +262,10 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
         __builtin_amdgcn_s_waitcnt(LGKM0);
         if (!(ABL & 4)) bar();
       }
-      if (a_dma_slot(s) && !(ABL & 1)) dma_go(dra, voa[(s - 24) / 5]);
+      if (a_dma_slot(s) && !(ABL & 1)) {
+        if constexpr ((ABL & 4096) != 0) gdma_go(gpa, voa[(s - 24) / 5]);
+        else dma_go(dra, voa[(s - 24) / 5]);
+      }
       // m0 for the next slot's piece, one MFMA ahead (the bare load then issues without a wait state)
       if (a_dma_slot(s + 1) && !(ABL & 1)) set_m0(dlds + (uint32_t)((s + 1 - 24) / 5) * PS);
       if (s == 40) hook();
@@ -278,7 +288,10 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
         if (r < 8) rd_a(nxt, 0, r, fa0);
         else rd_b(nxt, 0, r - 8, fb0);
       }
-      if (b_dma_slot(s) && !(ABL & 1)) dma_go(drb, vob[(s - 3) / 4]);
+      if (b_dma_slot(s) && !(ABL & 1)) {
+        if constexpr ((ABL & 4096) != 0) gdma_go(gpb, vob[(s - 3) / 4]);
+        else dma_go(drb, vob[(s - 3) / 4]);
+      }
       if (b_dma_slot(s + 1) && !(ABL & 1)) set_m0(dlds + OPB + (uint32_t)((s + 1 - 3) / 4) * PS);
       if (s == 30) hook();
       if constexpr (L) {
@@ -311,6 +324,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
   Pos p2;  // K-tile i + 2: the DMA target of iteration i
   pos_init(p2, 2);
   __amdgpu_buffer_rsrc_t dA = rs_a(p2);
+  if constexpr ((ABL & 4096) != 0) gpa = A + ((p2.lt < my_tiles) ? (int64_t)p2.m0 * lda + (int64_t)p2.kt * TK : 0);
   constexpr int NST_TAIL = nst_tail();
   // FIRST: the tile's first K-tile (zero-input MFMAs); LAST: its last, with the epilogue woven into its
   // second phase (OVL).  after_epi: 1 the previous iteration was a LAST one, 2 the between-tile
@@ -321,6 +335,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
     __amdgpu_buffer_rsrc_t dB;
     phase1(FIRST, cur, dA, dlds, [&]() __attribute__((always_inline)) {
       dB = rs_b(p2);
+      if constexpr ((ABL & 4096) != 0) gpb = B + ((p2.lt < my_tiles) ? (int64_t)p2.n0 * ldb + (int64_t)p2.kt * TK : 0);
       if constexpr (decltype(FIRST)::value) coords(first + (i / nk) * G, pm0, pn0);  // this tile's epilogue
     });
     __builtin_amdgcn_s_waitcnt(LGKM0);
@@ -332,6 +347,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
     phase2(LAST, nxt, dB, dlds, [&]() __attribute__((always_inline)) {
       pos_next(p2);
       dA = rs_a(p2);
+      if constexpr ((ABL & 4096) != 0) gpa = A + ((p2.lt < my_tiles) ? (int64_t)p2.m0 * lda + (int64_t)p2.kt * TK : 0);
     });
     __builtin_amdgcn_s_waitcnt(LGKM0);
   };
@@ -408,6 +424,7 @@ int launch_w128(const void* A, const void* B, void* C, int M, int N, int K, int6
       case 8: return launch_w128_v<EPI, 2, false, 8>(A, B, C, M, N, K, lda, ldb, ldc, s);
       case 16: return launch_w128_v<EPI, 2, false, 16>(A, B, C, M, N, K, lda, ldb, ldc, s);
       case 31: return launch_w128_v<EPI, 2, false, 31>(A, B, C, M, N, K, lda, ldb, ldc, s);
+      case 4096: return launch_w128_v<EPI, 2, true, 4096>(A, B, C, M, N, K, lda, ldb, ldc, s);
       default: break;
     }
   }

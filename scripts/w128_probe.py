@@ -63,7 +63,7 @@ def main():
                 G.set_w128_ablation(v)
                 res.setdefault((nm, f"w{v}"), []).append(timed(lambda: G.gemm_w128(x, w, out)))
             G.set_w128_ablation(0)
-    for v in [v for v in abl if v & (32 | 64 | 256 | 512 | 1024 | 2048) and not v & (31 | 128)]:  # the correct-result variants: numerics against hipBLASLt
+    for v in [v for v in abl if v & (32 | 64 | 256 | 512 | 1024 | 2048 | 4096) and not v & (31 | 128)]:  # the correct-result variants: numerics against hipBLASLt
         G.set_w128_ablation(v)
         for nm, (x, w, out, fl) in data.items():
             ref = torch.mm(x, w.t()).float()
