@@ -96,6 +96,13 @@ __device__ __forceinline__ void dma(__amdgpu_buffer_rsrc_t r, uint32_t voff, uin
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds) : "memory");
 }
+// FLAT-global form (SGPR base + 32-bit per-lane offset, no range check): only for half-tiles whose rows
+// all exist (ABL 1024)
+__device__ __forceinline__ void gdma(const void* base, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(base), "s"(lds) : "memory");
+}
 // accumulator pinned to AGPRs (tied operand): the chain on one accumulator needs no wait states;
 // compiler code reading the result waits for drain()
 #ifndef ND_PP_ASM_MFMA
@@ -365,7 +372,8 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
   }
 
 // ABL: ablation / A-B builds for profiling only (1-8, 16, 64, 128: wrong results): 1 no LDS-DMA in the
-// loop, 2 fragments read only in each tile's first K-tile, 4 no barriers in the loop, 8 no epilogue stores
+// loop, 2 fragments read only in each tile's first K-tile, 4 no barriers in the loop, 8 no epilogue stores;
+// 1024 (correct): full half-tiles staged with FLAT-global LDS loads instead of buffer loads
 template <int EPI, int HD, int ABL = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                          bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
@@ -445,17 +453,30 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
     const uint32_t dst = lds0 + (uint32_t)(s & 1) * BUF_B + 2 * HALF_B + (uint32_t)wn * 1024u;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const auto r = b_rsrc(p.n0, p.kt, h);
+      const bool full = EPI == PP_SWIGLU ? p.n0 + 128 <= N : p.n0 + 128 * h + 128 <= N;
+      if ((ABL & 1024) && full) {
+        const bf16_t* base = B + (int64_t)(p.n0 + (EPI == PP_SWIGLU ? 64 : 128) * h) * ldb + (int64_t)p.kt * TK;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dma(r, voff[q], dst + (uint32_t)h * HALF_B + (uint32_t)q * 4096u);
+        for (int q = 0; q < 4; ++q) gdma(base, voff[q], dst + (uint32_t)h * HALF_B + (uint32_t)q * 4096u);
+      } else {
+        const auto r = b_rsrc(p.n0, p.kt, h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dma(r, voff[q], dst + (uint32_t)h * HALF_B + (uint32_t)q * 4096u);
+      }
     }
   };
   // group 1: A half h of stream position p
   auto stage_a = [&](const Pos& p, int s, int h) __attribute__((always_inline)) {
     const uint32_t dst = lds0 + (uint32_t)(s & 1) * BUF_B + (uint32_t)h * HALF_B + (uint32_t)wn * 1024u;
-    const auto r = a_rsrc(p.m0, p.kt, h);
+    if ((ABL & 1024) && p.m0 + 128 * h + 128 <= M) {
+      const bf16_t* base = A + (int64_t)(p.m0 + 128 * h) * lda + (int64_t)p.kt * TK;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dma(r, voff[q], dst + (uint32_t)q * 4096u);
+      for (int q = 0; q < 4; ++q) gdma(base, voff[q], dst + (uint32_t)q * 4096u);
+    } else {
+      const auto r = a_rsrc(p.m0, p.kt, h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dma(r, voff[q], dst + (uint32_t)q * 4096u);
+    }
   };
 
   // ---- fragment reads: A rows 16 a + (lane & 15) of half g, B rows (wn & 1) 64 + 16 b + (lane & 15) of
@@ -637,6 +658,7 @@ int launch_pp_v(const void* A, const void* B, void* C, int M, int N, int K, int6
 template <int EPI, int HD = 64>
 int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
               const PPEpi& ep, hipStream_t s) {
+  if (g_pp_variant == 1024) return launch_pp_v<EPI, HD, 1024>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
   if constexpr (EPI == PP_STORE) {
     switch (g_pp_variant) {
       case 1: return launch_pp_v<EPI, HD, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);

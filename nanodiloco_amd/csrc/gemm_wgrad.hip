@@ -665,6 +665,12 @@ __device__ __forceinline__ void wpp_dma(__amdgpu_buffer_rsrc_t r, uint32_t voff,
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds) : "memory");
 }
+// FLAT-global form (SGPR base + 32-bit per-lane offset, no range check): half-tiles whose 128 columns exist
+__device__ __forceinline__ void wpp_gdma(const void* base, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(base), "s"(lds) : "memory");
+}
 __device__ __forceinline__ void wpp_bar() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -680,6 +686,7 @@ __device__ __forceinline__ void wpp_vmn(int n) {  // n in {0, 4, 8}
 }
 }  // namespace
 
+template <bool GD>
 __global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                           float* __restrict__ C, float* __restrict__ slab, int M, int N,
                                                           int K, int64_t lda, int64_t ldb, int64_t ldc, int S, int kchunk) {
@@ -710,11 +717,16 @@ __global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restri
   // half h of operand (g == 0: B columns n0 + 128 h .., g == 1: A columns m0 + 128 h ..) of K-tile kt
   auto stage = [&](int kt, int h) __attribute__((always_inline)) {
     const int64_t e0 = (int64_t)(kbeg + 64 * kt) * ld + (g == 0 ? n0 : m0) + 128 * h;
-    const auto r = wpp_rsrc((g == 0 ? B : A) + e0, ((int64_t)K * ld - e0) * 2);
     const uint32_t dst = lds0 + (uint32_t)(kt & 1) * WPP_BUF_B + (uint32_t)(g == 0 ? 2 + h : h) * WPP_HALF_B +
                          (uint32_t)wn * 1024u;
+    if (GD && (g == 0 ? n0 + 128 * h + 128 <= N : m0 + 128 * h + 128 <= M)) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) wpp_dma(r, voff[q], dst + (uint32_t)q * 4096u);
+      for (int q = 0; q < 4; ++q) wpp_gdma((g == 0 ? B : A) + e0, voff[q], dst + (uint32_t)q * 4096u);
+    } else {
+      const auto r = wpp_rsrc((g == 0 ? B : A) + e0, ((int64_t)K * ld - e0) * 2);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wpp_dma(r, voff[q], dst + (uint32_t)q * 4096u);
+    }
   };
   bf16x8 fa[8][2], fb[4][2];
   auto load_frags = [&](int kt) __attribute__((always_inline)) {
@@ -882,11 +894,19 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
     const int kchunk = fit_kchunk(K, &S, 64);
     const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
     const size_t lds = 2 * (size_t)WPP_BUF_B;  // 128 KiB
-    static const hipError_t attrp = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel),
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    static const hipError_t attrp =
+        (hipError_t)(hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<false>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) |
+                     hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<true>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (attrp != hipSuccess) return (int)attrp;
-    hipLaunchKernelGGL(wgrad_pp_kernel, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B, C, slab,
-                       M, N, K, lda, ldb, ldc, S, kchunk);
+    // "g": full half-tiles staged with FLAT-global LDS loads (A/B)
+    if (ev && ev[0] == 'g')
+      hipLaunchKernelGGL(wgrad_pp_kernel<true>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
+                         C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
+    else
+      hipLaunchKernelGGL(wgrad_pp_kernel<false>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
+                         C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
   } else if (large && variant == 5 && M >= 8 && N >= 8 && K % BK3 == 0) {  // "4w": 4-wave, AGPR-pinned accumulators
     const int kchunk = fit_kchunk(K, &S, BK3);
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
