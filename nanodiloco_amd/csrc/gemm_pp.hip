@@ -96,8 +96,8 @@ __device__ __forceinline__ void dma(__amdgpu_buffer_rsrc_t r, uint32_t voff, uin
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds) : "memory");
 }
-// FLAT-global form (SGPR base + 32-bit per-lane offset, no range check): only for half-tiles whose rows
-// all exist (ABL 1024)
+// FLAT-global form (SGPR base + 32-bit per-lane offset, no range check): the default for half-tiles whose rows
+// all exist (tail half-tiles keep the range-checked buffer form)
 __device__ __forceinline__ void gdma(const void* base, uint32_t voff, uint32_t lds) {
   uint32_t keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
@@ -373,7 +373,8 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
 
 // ABL: ablation / A-B builds for profiling only (1-8, 16, 64, 128: wrong results): 1 no LDS-DMA in the
 // loop, 2 fragments read only in each tile's first K-tile, 4 no barriers in the loop, 8 no epilogue stores;
-// 1024 (correct): full half-tiles staged with FLAT-global LDS loads instead of buffer loads
+// 1024 (correct): every half-tile staged with buffer loads (the default stages full half-tiles with FLAT-global
+// LDS loads: bitwise the same, 1.004-1.011x on the fused kernels, profiles/r4_gdma_ab.md)
 template <int EPI, int HD, int ABL = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                          bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
@@ -454,7 +455,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const bool full = EPI == PP_SWIGLU ? p.n0 + 128 <= N : p.n0 + 128 * h + 128 <= N;
-      if ((ABL & 1024) && full) {
+      if (!(ABL & 1024) && full) {
         const bf16_t* base = B + (int64_t)(p.n0 + (EPI == PP_SWIGLU ? 64 : 128) * h) * ldb + (int64_t)p.kt * TK;
 #pragma unroll
         for (int q = 0; q < 4; ++q) gdma(base, voff[q], dst + (uint32_t)h * HALF_B + (uint32_t)q * 4096u);
@@ -468,7 +469,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
   // group 1: A half h of stream position p
   auto stage_a = [&](const Pos& p, int s, int h) __attribute__((always_inline)) {
     const uint32_t dst = lds0 + (uint32_t)(s & 1) * BUF_B + (uint32_t)h * HALF_B + (uint32_t)wn * 1024u;
-    if ((ABL & 1024) && p.m0 + 128 * h + 128 <= M) {
+    if (!(ABL & 1024) && p.m0 + 128 * h + 128 <= M) {
       const bf16_t* base = A + (int64_t)(p.m0 + 128 * h) * lda + (int64_t)p.kt * TK;
 #pragma unroll
       for (int q = 0; q < 4; ++q) gdma(base, voff[q], dst + (uint32_t)q * 4096u);

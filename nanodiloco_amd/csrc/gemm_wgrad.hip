@@ -900,8 +900,9 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
                      hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<true>),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (attrp != hipSuccess) return (int)attrp;
-    // "g": full half-tiles staged with FLAT-global LDS loads (A/B)
-    if (ev && ev[0] == 'g')
+    // default: full half-tiles staged with FLAT-global LDS loads (bitwise the same as the buffer form,
+    // 1.005x over the three Llama-150M shapes, profiles/r4_gdma_ab.md); "b": buffer loads only (A/B)
+    if (!(ev && ev[0] == 'b'))
       hipLaunchKernelGGL(wgrad_pp_kernel<true>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
                          C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
     else

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of the LDS-DMA piece form in the step's own GEMMs: buffer_load ... lds (V#, range-checked) vs
-global_load_lds (SGPR base + per-lane offset) for full half-tiles.  Fused ping-pong kernels (gemm_pp.hip
-variant 1024) and the weight-gradient kernel (gemm_wgrad.hip, ND_WGRAD_VARIANT=g), Llama-150M shapes at
+global_load_lds (SGPR base + per-lane offset, the default) for full half-tiles.  Fused ping-pong kernels
+(gemm_pp.hip variant 1024 = buffer form) and the weight-gradient kernel (gemm_wgrad.hip, ND_WGRAD_VARIANT=b), Llama-150M shapes at
 --tokens.  Checks the two forms produce bitwise-equal outputs, then times them interleaved.
 
     python scripts/gdma_ab.py [--tokens 131072] [--rounds 5]
@@ -62,11 +62,11 @@ def main():
     def arm(name, flat):
         if name.startswith("wgrad"):
             if flat:
-                os.environ["ND_WGRAD_VARIANT"] = "g"
-            else:
                 os.environ.pop("ND_WGRAD_VARIANT", None)
+            else:
+                os.environ["ND_WGRAD_VARIANT"] = "b"
         else:
-            G.set_pp_variant(1024 if flat else 0)
+            G.set_pp_variant(0 if flat else 1024)
 
     bad = 0
     for name, (fl, fn) in cases.items():
@@ -93,8 +93,8 @@ def main():
             for flat in (False, True):
                 arm(name, flat)
                 res.setdefault((name, flat), []).append(timed(fn))
-    arm("wgrad", False)
-    arm("pp", False)
+    arm("wgrad", True)
+    arm("pp", True)
     tot = [0.0, 0.0]
     for name, (fl, fn) in cases.items():
         t = [sorted(res[(name, f)])[a.rounds // 2] for f in (False, True)]
