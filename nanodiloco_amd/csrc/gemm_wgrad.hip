@@ -686,7 +686,9 @@ __device__ __forceinline__ void wpp_vmn(int n) {  // n in {0, 4, 8}
 }
 }  // namespace
 
-template <bool GD>
+// ABL (timing ablations, wrong results; ND_WGRAD_VARIANT=a<bits>): 1 no LDS-DMA in the loop, 2 fragments read
+// only for the first K-tile, 4 no barriers in the loop, 8 no vmcnt waits in the loop, 16 no MFMAs
+template <bool GD, int ABL = 0>
 __global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                           float* __restrict__ C, float* __restrict__ slab, int M, int N,
                                                           int K, int64_t lda, int64_t ldb, int64_t ldc, int S, int kchunk) {
@@ -762,7 +764,8 @@ __global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restri
   for (int s = 0; s < nk; ++s) {
     const bool more1 = s + 1 < nk, more2 = s + 2 < nk;
     // ================= LOAD(s)
-    if (g == 0) {
+    if (ABL & 1) {
+    } else if (g == 0) {
       if (more1) {
         stage(s + 1, 0);
         stage(s + 1, 1);
@@ -771,23 +774,32 @@ __global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restri
       if (more1) stage(s + 1, 1);  // A1(s + 1)
       if (more2) stage(s + 2, 0);  // A0(s + 2)
     }
-    load_frags(s);
+    if (!(ABL & 2) || s == 0) load_frags(s);
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    if (g == 1) wpp_vmn((more1 ? 4 : 0) + (more2 ? 4 : 0));  // A0(s + 1) landed
-    wpp_bar();
+    if (g == 1 && !(ABL & 8)) wpp_vmn((more1 ? 4 : 0) + (more2 ? 4 : 0));  // A0(s + 1) landed
+    if (!(ABL & 4)) wpp_bar();
     // ================= COMPUTE(s)
     __builtin_amdgcn_s_setprio(1);
+    if constexpr ((ABL & 16) != 0) {
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) asm volatile("" ::"v"(fa[a][0]), "v"(fb[b][1]));
+    } else {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int a = 0; a < 8; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = wpp_mma(fa[a][ks], fb[b][ks], acc[a][b]);
+    }
     __builtin_amdgcn_s_setprio(0);
-    if (g == 0) wpp_vm<0>();            // B(s + 1) landed
+    if (ABL & 8) {
+    } else if (g == 0) wpp_vm<0>();     // B(s + 1) landed
     else wpp_vmn(more2 ? 4 : 0);        // A1(s + 1) landed
-    wpp_bar();
+    if (!(ABL & 4)) wpp_bar();
   }
+  if (ABL & 9) wpp_vm<0>();
   // epilogue: acc[a][b] lane l reg r = C[m0 + 128 g + 16 a + 4 (l >> 4) + r][n0 + 64 wn + 16 b + (l & 15)].
   // Both groups first meet at the same barrier (group 1 ran one more), after which every LDS read and
   // LDS-DMA write of the K-loop is done; each wave then transposes its 128 x 64 block through a private
@@ -900,6 +912,16 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
                      hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<true>),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (attrp != hipSuccess) return (int)attrp;
+    if (ev && ev[0] == 'a') {  // timing ablations (wrong results)
+      const int abl = atoi(ev + 1);
+#define ND_WA(X) case X: hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<true, X>), \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+  hipLaunchKernelGGL((wgrad_pp_kernel<true, X>), dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, \
+                     (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk); break;
+      switch (abl) { ND_WA(1) ND_WA(2) ND_WA(4) ND_WA(8) ND_WA(16) ND_WA(3) ND_WA(7) ND_WA(15) ND_WA(31) default: return (int)hipErrorInvalidValue; }
+#undef ND_WA
+      ND_LAUNCH_CHECK();
+    }
     // default: full half-tiles staged with FLAT-global LDS loads (bitwise the same as the buffer form,
     // 1.005x over the three Llama-150M shapes, profiles/r4_gdma_ab.md); "b": buffer loads only (A/B)
     if (!(ev && ev[0] == 'b'))
