@@ -638,7 +638,12 @@ int num_cus_pp() {
   return n;
 }
 
-int g_pp_variant = 0;  // ablation builds (profiling only, wrong results): nd_gemm_pp_set_variant
+// ablation / A-B builds: nd_gemm_pp_set_variant or ND_GEMM_PP_VARIANT (1024 = buffer-form pieces, correct;
+// the others are timing-only builds with wrong results)
+int g_pp_variant = [] {
+  const char* e = getenv("ND_GEMM_PP_VARIANT");
+  return e ? atoi(e) : 0;
+}();
 
 
 template <int EPI, int HD, int ABL>
