@@ -78,6 +78,8 @@ struct PPEpi {
   int64_t ld_act;
   const bf16_t* gu;   // PP_DSWIGLU: gu [M, 2F]
   int64_t ld_gu;
+  const float* sa;    // fp8 operands (F8 != 0): per-tensor dequantisation scales, acc *= sa[0] * sb[0]
+  const float* sb;
 };
 
 // stores per wave per tile epilogue (counted by the vmcnt waits that follow it)
@@ -121,6 +123,24 @@ __device__ __forceinline__ void mma0(const bf16x8& a, const bf16x8& b, f32x4& c)
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
 }
 #endif
+// fp8 operands (F8 1: A e4m3, B e4m3; 2: A e5m2, B e4m3): one 16x16x128 MFMA on the two 16-B halves of
+// each fragment (the lane's 32 K bytes), unit E8M0 block scales (`one` = 0x7F7F7F7F).  The MFMA's first
+// source is B (cbsz = B's format), its second A (blgp = A's format).
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ i32x8 cat16(const bf16x8& x, const bf16x8& y) {
+  const i32x4 a = __builtin_bit_cast(i32x4, x), b = __builtin_bit_cast(i32x4, y);
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+template <int F8>
+__device__ __forceinline__ void mma8(const i32x8& b, const i32x8& a, f32x4& c, int one) {
+  c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b, a, c, 0, F8 == 1 ? 0 : 1, 0, one, 0, one);
+}
+template <int F8>
+__device__ __forceinline__ void mma8z(const i32x8& b, const i32x8& a, f32x4& c, int one) {
+  c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b, a, f32x4{0.f, 0.f, 0.f, 0.f}, 0, F8 == 1 ? 0 : 1, 0, one, 0,
+                                                         one);
+}
 __device__ __forceinline__ void drain() { asm volatile("s_nop 15\n\ts_nop 3" ::: "memory"); }
 __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
@@ -160,10 +180,10 @@ __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); 
 // of the tile at (m0, n0) -> the fused output(s).  Exactly NStores<EPI> 16-B buffer stores per wave
 // (the callers' counted waits rely on it); out-of-range lanes drop through the descriptor's record
 // count or an offset sentinel.  `smem` + 2 BUF_B + 4 KiB w: the wave's private C staging region.
-template <int EPI, int HD, int ABL>
+template <int EPI, int HD, int ABL, int F8 = 0>
 __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __restrict__ C, int M, int N,
                                             int64_t ldc, const PPEpi& ep, int m0, int n0, int g, int wn, int w,
-                                            int lane, char* smem) {
+                                            int lane, char* smem, float sc) {
   constexpr int STP = (ABL & 32) ? 0 : 2;
 
     // per-lane row offsets derive from an opaque zero: otherwise LICM hoists every row's store
@@ -198,6 +218,10 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
           }
         }
         f32x4 v[4] = {acc[a][0], acc[a][1], acc[a][2], acc[a][3]};
+        if constexpr (F8 != 0) {
+#pragma unroll
+          for (int b = 0; b < 4; ++b) v[b] *= sc;
+        }
         if constexpr (EPI == PP_ROPE) {
           // the wave's 64 columns are one 64-wide head (or two 32-wide ones): column block b pairs
           // with b + HD / 32 in the same lane; v columns (>= rope_cols) pass through
@@ -266,8 +290,8 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            g2[j][r] = rbf(acc[a][j][r]);  // act from the rounded gate / up: what the backward reads
-            u2[j][r] = rbf(acc[a][j + 2][r]);
+            g2[j][r] = rbf(F8 != 0 ? acc[a][j][r] * sc : acc[a][j][r]);  // act from the rounded gate / up: what the backward reads
+            u2[j][r] = rbf(F8 != 0 ? acc[a][j + 2][r] * sc : acc[a][j + 2][r]);
             y2[j][r] = silu(g2[j][r]) * u2[j][r];
           }
         const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
@@ -322,6 +346,10 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
                                                               __float_as_uint(acc[a][2 * bp + 1][r]), false, false);
             d0[r] = __uint_as_float(sw[0]);
             d1[r] = __uint_as_float(sw[1]);
+            if constexpr (F8 != 0) {
+              d0[r] *= sc;
+              d1[r] *= sc;
+            }
           }
           // lane row q even: d0 = units 0-3, d1 = units 4-7 of block 2 bp (cols 8 (q >> 1) ..);
           // odd: d0 = block 2 bp + 1's units 0-3 ... -- the same (x, y) order pair16 packs
@@ -375,11 +403,17 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
 // loop, 2 fragments read only in each tile's first K-tile, 4 no barriers in the loop, 8 no epilogue stores;
 // 1024 (correct): every half-tile staged with buffer loads (the default stages full half-tiles with FLAT-global
 // LDS loads: bitwise the same, 1.004-1.011x on the fused kernels, profiles/r4_gdma_ab.md)
-template <int EPI, int HD, int ABL = 0>
-__global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+// F8 (fp8 operands, one 16x16x128 MFMA per 128-deep K-tile of the same 128-B LDS rows): 0 bf16; 1 A e4m3,
+// B e4m3 (forward); 2 A e5m2, B e4m3 (input gradient).  A / B are then byte arrays, lda / ldb in bytes.
+template <int EPI, int HD, int ABL = 0, int F8 = 0>
+__global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restrict__ A_, const bf16_t* __restrict__ B_,
                                                          bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
                                                          int64_t ldb, int64_t ldc, PPEpi ep, int GM) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int ES = F8 ? 1 : 2;       // operand bytes per element
+  constexpr int TKE = TK * 2 / ES;     // operand elements per K-tile (128 B per row either way)
+  const char* __restrict__ A = reinterpret_cast<const char*>(A_);
+  const char* __restrict__ B = reinterpret_cast<const char*>(B_);
   constexpr int NST = NStores<EPI>::v;
   // C stores: non-temporal (aux 2) and, for the plain / RoPE epilogues, full 128-B lines staged
   // through LDS (measured -6 % kernel time together, profiles/r3_gemm_pp.md); ABL 32 / 256 turn
@@ -390,12 +424,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
   const int G = gridDim.x;  // <= tiles (host)
   const int first = xcd_remap(blockIdx.x, G);
   const int my_tiles = (tiles - 1 - first) / G + 1;
-  const int nk = K / TK;
+  const int nk = K / TKE;
   const int total = my_tiles * nk;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = w >> 2, wn = w & 3;
   const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  const float sc = F8 != 0 ? ep.sa[0] * ep.sb[0] : 1.f;  // fp8 dequantisation of the accumulator
+  int one = 0;  // unit E8M0 block scales of the fp8 MFMA
+  if constexpr (F8 != 0) asm volatile("v_mov_b32 %0, 0x7f7f7f7f" : "=v"(one));
 
   // tile t -> (m0, n0): groups of GM m-panels walked n-major inside the group
   auto coords = [&](int t, int& m0, int& n0) __attribute__((always_inline)) {
@@ -420,20 +457,20 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
     const int lch = (lane & 7) ^ ((hr >> 1) & 7);
     int row = hr;
     if (g == 0 && EPI == PP_SWIGLU) row = ((hr >> 5) & 1) * N + (hr >> 6) * 32 + (hr & 31);  // gate | up rows
-    voff[p] = (uint32_t)(((int64_t)row * (g == 0 ? ldb : lda) + lch * 8) * 2);
+    voff[p] = (uint32_t)((int64_t)row * (g == 0 ? ldb : lda) * ES + lch * 16);
   }
   // descriptor of one half-tile of K-tile kt of tile t: A half h (rows m0 + 128 h ..) or B half h
   auto a_rsrc = [&](int m0, int kt, int h) __attribute__((always_inline)) {
-    const int64_t e0 = (int64_t)(m0 + 128 * h) * lda + (int64_t)kt * TK;
-    const int64_t lim = (int64_t)M * lda - e0;  // elements to the end of the operand's last row
-    return rsrc(A + e0, (uint32_t)(lim > 0 ? (lim < 0x3fffffff ? lim * 2 : 0x7ffffffe) : 0));
+    const int64_t e0 = ((int64_t)(m0 + 128 * h) * lda + (int64_t)kt * TKE) * ES;
+    const int64_t lim = (int64_t)M * lda * ES - e0;  // bytes to the end of the operand's last row
+    return rsrc(A + e0, (uint32_t)(lim > 0 ? (lim < 0x7ffffffe ? lim : 0x7ffffffe) : 0));
   };
   auto b_rsrc = [&](int n0, int kt, int h) __attribute__((always_inline)) {
     const int64_t hrow = EPI == PP_SWIGLU ? 64 * h : 128 * h;  // SwiGLU: half 1 = wave groups 2, 3
-    const int64_t e0 = (int64_t)(n0 + hrow) * ldb + (int64_t)kt * TK;
+    const int64_t e0 = ((int64_t)(n0 + hrow) * ldb + (int64_t)kt * TKE) * ES;
     const int64_t rows = EPI == PP_SWIGLU ? 2 * (int64_t)N : N;
-    const int64_t lim = rows * ldb - e0;
-    return rsrc(B + e0, (uint32_t)(lim > 0 ? (lim < 0x3fffffff ? lim * 2 : 0x7ffffffe) : 0));
+    const int64_t lim = rows * ldb * ES - e0;
+    return rsrc(B + e0, (uint32_t)(lim > 0 ? (lim < 0x7ffffffe ? lim : 0x7ffffffe) : 0));
   };
   // stream positions -> (tile, kt): incremental counters
   struct Pos { int lt, kt, m0, n0; };
@@ -456,7 +493,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
     for (int h = 0; h < 2; ++h) {
       const bool full = EPI == PP_SWIGLU ? p.n0 + 128 <= N : p.n0 + 128 * h + 128 <= N;
       if (!(ABL & 1024) && full) {
-        const bf16_t* base = B + (int64_t)(p.n0 + (EPI == PP_SWIGLU ? 64 : 128) * h) * ldb + (int64_t)p.kt * TK;
+        const char* base = B + ((int64_t)(p.n0 + (EPI == PP_SWIGLU ? 64 : 128) * h) * ldb + (int64_t)p.kt * TKE) * ES;
 #pragma unroll
         for (int q = 0; q < 4; ++q) gdma(base, voff[q], dst + (uint32_t)h * HALF_B + (uint32_t)q * 4096u);
       } else {
@@ -470,7 +507,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
   auto stage_a = [&](const Pos& p, int s, int h) __attribute__((always_inline)) {
     const uint32_t dst = lds0 + (uint32_t)(s & 1) * BUF_B + (uint32_t)h * HALF_B + (uint32_t)wn * 1024u;
     if (!(ABL & 1024) && p.m0 + 128 * h + 128 <= M) {
-      const bf16_t* base = A + (int64_t)(p.m0 + 128 * h) * lda + (int64_t)p.kt * TK;
+      const char* base = A + ((int64_t)(p.m0 + 128 * h) * lda + (int64_t)p.kt * TKE) * ES;
 #pragma unroll
       for (int q = 0; q < 4; ++q) gdma(base, voff[q], dst + (uint32_t)q * 4096u);
     } else {
@@ -483,8 +520,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
   // ---- fragment reads: A rows 16 a + (lane & 15) of half g, B rows (wn & 1) 64 + 16 b + (lane & 15) of
   // half 2 + (wn >> 1); chunk (4 ks + lane / 16) ^ swizzle -- the same per-lane offset for A and B
   const int r16 = lane & 15, q = lane >> 4;
-  const uint32_t foff0 = (uint32_t)(r16 * 128 + ((q ^ ((r16 >> 1) & 7)) << 4));
-  const uint32_t foff1 = (uint32_t)(r16 * 128 + (((4 + q) ^ ((r16 >> 1) & 7)) << 4));
+  // bf16: k-step 0 = chunk q, k-step 1 = chunk 4 + q; fp8: the lane's 32 K bytes = chunks 2 q, 2 q + 1
+  const int ch0 = F8 ? 2 * q : q, ch1 = F8 ? 2 * q + 1 : 4 + q;
+  const uint32_t foff0 = (uint32_t)(r16 * 128 + ((ch0 ^ ((r16 >> 1) & 7)) << 4));
+  const uint32_t foff1 = (uint32_t)(r16 * 128 + ((ch1 ^ ((r16 >> 1) & 7)) << 4));
   bf16x8 fa[8][2], fb[4][2];
   auto load_frags = [&](int s) __attribute__((always_inline)) {
     const char* base = smem + (s & 1) * BUF_B;
@@ -576,7 +615,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
       } else {
         int m0, n0;
         coords(first + (lt - 1) * G, m0, n0);
-        pp_epilogue<EPI, HD, ABL>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem);
+        pp_epilogue<EPI, HD, ABL, F8>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc);
       }
       // the accumulators are free only after the epilogue has read them: keep the fragment reads
       // (96 VGPRs) from being hoisted into it
@@ -590,6 +629,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
     if (!(ABL & 4)) bar();
     // ================= COMPUTE(s)
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (F8 != 0) {
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if constexpr (F) mma8z<F8>(cat16(fb[b][0], fb[b][1]), cat16(fa[a][0], fa[a][1]), acc[a][b], one);
+          else mma8<F8>(cat16(fb[b][0], fb[b][1]), cat16(fa[a][0], fa[a][1]), acc[a][b], one);
+        }
+    } else {
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
@@ -601,6 +649,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
     for (int a = 0; a < 8; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) mma(fb[b][1], fa[a][1], acc[a][b]);
+    }
     __builtin_amdgcn_s_setprio(0);
     if (ABL & 16) {
     } else if (g == 0) {
@@ -618,7 +667,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
   if constexpr ((ABL & 8) == 0) {
     int m0, n0;
     coords(first + (my_tiles - 1) * G, m0, n0);
-    pp_epilogue<EPI, HD, ABL>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem);
+    pp_epilogue<EPI, HD, ABL, F8>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc);
   }
   if (g == 0 && !(ABL & 4)) bar();  // group 1 ran one barrier more
 }
@@ -646,17 +695,17 @@ int g_pp_variant = [] {
 }();
 
 
-template <int EPI, int HD, int ABL>
+template <int EPI, int HD, int ABL, int F8 = 0>
 int launch_pp_v(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
                 const PPEpi& ep, hipStream_t s) {
   const size_t lds = 2 * (size_t)BUF_B + ((ABL & 256) ? 0 : 8 * 4096);  // 128 KiB + 32 KiB C staging
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<EPI, HD, ABL>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<EPI, HD, ABL, F8>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return (int)attr;
   const int tcols = EPI == PP_SWIGLU ? 128 : TN;
   const int tiles = ((M + TM - 1) / TM) * ((N + tcols - 1) / tcols);
   const int grid = tiles < num_cus_pp() ? tiles : num_cus_pp();
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, HD, ABL>), dim3(grid), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, HD, ABL, F8>), dim3(grid), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
                      (bf16_t*)C, M, N, K, lda, ldb, ldc, ep, g_pp_group_m);
   ND_LAUNCH_CHECK();
 }
@@ -737,6 +786,64 @@ ND_API int nd_gemm_pp_dswiglu(const void* A, const void* B, const void* gu, void
   PPEpi ep{};
   ep.gu = (const bf16_t*)gu; ep.ld_gu = ld_gu;
   return launch_pp<PP_DSWIGLU>(A, B, dgu, M, F, K, lda, ldb, ld_dgu, ep, s);
+}
+
+// ---- fp8 operands (A, B byte arrays, lda / ldb in bytes = elements): C = bf16(sa sb A . B^T) and the same
+// fused epilogues on the dequantised accumulator.  fa: A's format (0 e4m3, 1 e5m2); B is e4m3.  K % 128 == 0.
+namespace {
+bool pp_f8_ok(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int fa, const float* sa, const float* sb) {
+  return M > 0 && N > 0 && K > 0 && K % 128 == 0 && N % 8 == 0 && lda % 16 == 0 && ldb % 16 == 0 && ldc % 8 == 0 &&
+         lda >= K && ldb >= K && (int64_t)TM * lda < (1ll << 31) && (int64_t)TN * ldb < (1ll << 31) &&
+         (int64_t)TM * ldc * 2 < (1ll << 31) && (fa == 0 || fa == 1) && sa && sb;
+}
+template <int EPI, int HD = 64>
+int launch_pp8(int fa, const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
+               const PPEpi& ep, hipStream_t s) {
+  return fa == 0 ? launch_pp_v<EPI, HD, 0, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s)
+                 : launch_pp_v<EPI, HD, 0, 2>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+}
+}  // namespace
+
+ND_API int nd_gemm_pp_f8(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                         int64_t ldc, const float* sa, const float* sb, int fa, hipStream_t s) {
+  if (!pp_f8_ok(M, N, K, lda, ldb, ldc, fa, sa, sb)) return (int)hipErrorInvalidValue;
+  PPEpi ep{};
+  ep.sa = sa; ep.sb = sb;
+  return launch_pp8<PP_STORE>(fa, A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+}
+
+ND_API int nd_gemm_pp_rope_f8(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                              int64_t ldc, const float* sa, const float* sb, const float* cosT, const float* sinT, int T,
+                              int hd, int rope_cols, hipStream_t s) {
+  if (!pp_f8_ok(M, N, K, lda, ldb, ldc, 0, sa, sb) || (hd != 32 && hd != 64) || rope_cols % 64 || T <= 0)
+    return (int)hipErrorInvalidValue;
+  PPEpi ep{};
+  ep.cosT = cosT; ep.sinT = sinT; ep.T = T; ep.rope_cols = rope_cols; ep.sa = sa; ep.sb = sb;
+  return hd == 64 ? launch_pp_v<PP_ROPE, 64, 0, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s)
+                  : launch_pp_v<PP_ROPE, 32, 0, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+}
+
+ND_API int nd_gemm_pp_swiglu_f8(const void* A, const void* B, void* gu, void* act, int M, int F, int K, int64_t lda,
+                                int64_t ldb, int64_t ldc, int64_t ld_act, const float* sa, const float* sb,
+                                hipStream_t s) {
+  if (!pp_f8_ok(M, F, K, lda, ldb, ldc, 0, sa, sb) || ldc < 2 * (int64_t)F || ld_act % 8 || ld_act < F ||
+      (int64_t)2 * F * ldb >= (1ll << 31) || (int64_t)TM * ld_act * 2 >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  PPEpi ep{};
+  ep.act = (bf16_t*)act; ep.ld_act = ld_act; ep.sa = sa; ep.sb = sb;
+  return launch_pp_v<PP_SWIGLU, 64, 0, 1>(A, B, gu, M, F, K, lda, ldb, ldc, ep, s);
+}
+
+// A = dY in e5m2 (fa = 1) or e4m3 (fa = 0)
+ND_API int nd_gemm_pp_dswiglu_f8(const void* A, const void* B, const void* gu, void* dgu, int M, int F, int K,
+                                 int64_t lda, int64_t ldb, int64_t ld_gu, int64_t ld_dgu, const float* sa,
+                                 const float* sb, int fa, hipStream_t s) {
+  if (!pp_f8_ok(M, F, K, lda, ldb, ld_dgu, fa, sa, sb) || ld_gu % 8 || ld_gu < 2 * (int64_t)F ||
+      ld_dgu < 2 * (int64_t)F || (int64_t)TM * ld_gu * 2 >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  PPEpi ep{};
+  ep.gu = (const bf16_t*)gu; ep.ld_gu = ld_gu; ep.sa = sa; ep.sb = sb;
+  return launch_pp8<PP_DSWIGLU>(fa, A, B, dgu, M, F, K, lda, ldb, ld_dgu, ep, s);
 }
 
 ND_API int nd_gemm_pp_set_variant(int v) {

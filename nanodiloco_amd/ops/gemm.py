@@ -129,6 +129,68 @@ def gemm_pp_dswiglu(dy, w_down_t, gu, dgu_out=None):
     return dgu
 
 
+# ---- the same ping-pong kernels on fp8 operands (one v_mfma_scale_f32_16x16x128_f8f6f4 per 128-deep K-tile):
+# a e4m3 (forward) or e5m2 (input gradient), b e4m3; sa / sb one-element fp32 dequantisation scales
+# (the torch._scaled_mm contract); bf16 outputs and the fused epilogues on the dequantised accumulator.
+
+def pp_f8_supported(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return (a.is_cuda and _ext.get_backend() != "torch" and a.dim() == 2 and b.dim() == 2
+            and a.dtype in _F8_FMT and b.dtype == torch.float8_e4m3fn and a.shape[1] == b.shape[1]
+            and a.shape[1] % 128 == 0 and b.shape[0] % 8 == 0 and a.stride(1) == 1 and b.stride(1) == 1
+            and a.stride(0) % 16 == 0 and b.stride(0) % 16 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+
+
+def gemm_pp_f8(a, b, sa, sb, out=None) -> torch.Tensor:
+    """out[M, N] (bf16) = sa * sb * a[M, K] . b[N, K]^T."""
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_pp_f8(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0), b.stride(0),
+                                        out.stride(0), _ext.ptr(sa), _ext.ptr(sb), _F8_FMT[a.dtype],
+                                        _ext.stream_ptr(a.device)), "nd_gemm_pp_f8")
+    return out
+
+
+def gemm_pp_rope_f8(a, b, sa, sb, cos, sin, T: int, hd: int, rope_cols: int, out=None) -> torch.Tensor:
+    """fp8 q|k|v projection (a e4m3) with RoPE on the first ``rope_cols`` columns, bf16 out."""
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_pp_rope_f8(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0),
+                                             b.stride(0), out.stride(0), _ext.ptr(sa), _ext.ptr(sb), _ext.ptr(cos),
+                                             _ext.ptr(sin), T, hd, rope_cols, _ext.stream_ptr(a.device)),
+               "nd_gemm_pp_rope_f8")
+    return out
+
+
+def gemm_pp_swiglu_f8(a, w_gu, sa, sb, gu_out=None, act_out=None):
+    """fp8 gate|up projection (a, w_gu e4m3) + SwiGLU: (gu [M, 2F], act [M, F]) in bf16."""
+    M, K = a.shape
+    F = w_gu.shape[0] // 2
+    gu = gu_out if gu_out is not None else torch.empty(M, 2 * F, dtype=torch.bfloat16, device=a.device)
+    act = act_out if act_out is not None else torch.empty(M, F, dtype=torch.bfloat16, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_pp_swiglu_f8(_ext.ptr(a), _ext.ptr(w_gu), _ext.ptr(gu), _ext.ptr(act), M, F, K,
+                                               a.stride(0), w_gu.stride(0), gu.stride(0), act.stride(0),
+                                               _ext.ptr(sa), _ext.ptr(sb), _ext.stream_ptr(a.device)),
+               "nd_gemm_pp_swiglu_f8")
+    return gu, act
+
+
+def gemm_pp_dswiglu_f8(dy, w_down_t, sa, sb, gu, dgu_out=None):
+    """fp8 down-projection input gradient (dy e5m2 / e4m3, w_down_t e4m3) fused with the SwiGLU backward:
+    d(gate|up) [M, 2F] bf16."""
+    M, K = dy.shape
+    F = w_down_t.shape[0]
+    dgu = dgu_out if dgu_out is not None else torch.empty_like(gu)
+    _ext.check(_ext.lib().nd_gemm_pp_dswiglu_f8(_ext.ptr(dy), _ext.ptr(w_down_t), _ext.ptr(gu), _ext.ptr(dgu), M, F,
+                                                K, dy.stride(0), w_down_t.stride(0), gu.stride(0), dgu.stride(0),
+                                                _ext.ptr(sa), _ext.ptr(sb), _F8_FMT[dy.dtype],
+                                                _ext.stream_ptr(dy.device)), "nd_gemm_pp_dswiglu_f8")
+    return dgu
+
+
 def gemm_w128(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     """out[M, N] = a[M, K] . b[N, K]^T on the one-wave-per-SIMD kernel (csrc/gemm_w128.hip: 4 waves,
     128 x 128 outputs per wave, one continuous MFMA stream per K-tile -- the hipBLASLt K-loop shape)."""

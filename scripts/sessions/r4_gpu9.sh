@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 4, session 9: fp8 ping-pong GEMM -- numerics, then per-shape timing vs hipBLASLt fp8 and bf16
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${SESSION:-r4q}
+mkdir -p $O
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 400 python -u -m pytest tests/test_gemm_pp_f8_gpu.py -x -q --timeout 120 --timeout-method thread > $O/test.log 2>&1
+rc=$?; tail -15 $O/test.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u scripts/gemm_pp_f8_bench.py --rounds 5 > $O/bench.log 2>&1
+rc=$?; cat $O/bench.log; exit $rc
