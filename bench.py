@@ -82,8 +82,11 @@ def parse():
                     help="SwiGLU in the gate|up GEMM epilogue and its backward in the down dgrad epilogue")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
     ap.add_argument("--fp8-wgrad", action="store_true", help="with --fp8: weight-gradient GEMM in fp8 too")
-    ap.add_argument("--fp8-gemm", default="hipblaslt", choices=["hip", "hipblaslt"],
-                    help="with --fp8: forward / input-gradient fp8 GEMMs on our MFMA kernel or hipBLASLt")
+    ap.add_argument("--fp8-gemm", default="pp", choices=["pp", "hip", "hipblaslt"],
+                    help="with --fp8: forward / input-gradient fp8 GEMMs on the own ping-pong fp8 kernel (pp, "
+                         "default), the round-2 fp8 kernel (hip) or hipBLASLt")
+    ap.add_argument("--fp8-fused-epi", type=int, default=1, choices=[0, 1],
+                    help="with --fp8 and --fp8-gemm pp: RoPE / SwiGLU fused into the fp8 GEMM epilogues")
     ap.add_argument("--fp8-keep-fused", default="none", choices=["none", "rope", "mlp", "both"],
                     help="with --fp8: projections that stay on the bf16 fused-epilogue GEMMs")
     ap.add_argument("--fp8-fused-quant", type=int, default=1, choices=[0, 1],
@@ -103,6 +106,7 @@ def main():
         from nanodiloco_amd.ops import fp8 as _fp8
         _fp8.set_fused_quant(bool(a.fp8_fused_quant))
         _fp8.set_fp8_gemm(a.fp8_gemm)
+        _fp8.set_fp8_fused_epilogues(bool(a.fp8_fused_epi))
         _fp8.set_fp8_keep_fused(a.fp8_keep_fused)
     if a.wgrad_variant:
         os.environ["ND_WGRAD_VARIANT"] = a.wgrad_variant
@@ -237,6 +241,7 @@ def main():
             "proj_gemm": ops.proj_gemm(),
             "fused_epilogues": ops.fused_epilogues(),
             "fp8_gemm": a.fp8_gemm if a.fp8 else None,
+            "fp8_fused_epilogues": bool(a.fp8_fused_epi) if a.fp8 else None,
             "fp8_keep_fused": a.fp8_keep_fused if a.fp8 else None,
             "dgrad_transposed": ops.dgrad_transposed_enabled(),
             "ops": ops.get_backend() if a.ops != "auto" else ("hip" if env.device.type == "cuda" else "torch"),

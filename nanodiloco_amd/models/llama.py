@@ -200,6 +200,11 @@ class LlamaForCausalLM:
             # own GEMM with RoPE on q|k in its epilogue: the attention skips its rotation pass
             qkv = ops.linear_rope(y, w_qkv, self._fused(qn, "grad"), wt_qkv, cos, sin, T, c.head_dim, rope_cols)
             rotated = True
+        elif fp8_qkv and self.fp8.rope_ok(y, w_qkv, c.head_dim, rope_cols):
+            # the same on the own fp8 GEMM (e4m3 operands, RoPE on the dequantised accumulator)
+            qkv = self.fp8.rope(f"{i}.qkv", y, w_qkv, self._fused(qn, "grad"), self.store.version, y8, cos, sin, T,
+                                c.head_dim, rope_cols)
+            rotated = True
         else:
             qkv = self._linear(f"{i}.qkv", y, w_qkv, self._fused(qn, "grad"), y8)
             rotated = False
@@ -220,6 +225,12 @@ class LlamaForCausalLM:
                 m = ops.mlp_fused(y, w_gu, self._fused(gn, "grad"), wt_gu, w_dn,
                                   self._g(p + "mlp.down_proj.weight"), wt_dn)
                 return m, h
+        elif self.fp8.mlp_ok(y, w_gu, w_dn):
+            # the same fusion on the own fp8 GEMMs
+            m = self.fp8.mlp(f"{i}.gu", f"{i}.down", y, w_gu, w_dn, self._fused(gn, "grad"),
+                             self._g(p + "mlp.down_proj.weight"), self.store.version,
+                             q_gu.out if q_gu is not None else None)
+            return m, h
         q_down = self._q8(f"{i}.down")
         gu = self._linear(f"{i}.gu", y, w_gu, self._fused(gn, "grad"), q_gu.out if q_gu is not None else None)
         act = ops.swiglu(gu, q8=q_down, q8_bwd=self._q8(f"{i}.gu", grad=True))

@@ -30,7 +30,8 @@ from typing import Dict, Optional
 import torch
 
 from . import _ext
-from .gemm import f8_nt_supported, gemm_nt_f8, wgrad, wgrad_supported
+from .gemm import (f8_nt_supported, gemm_nt_f8, gemm_pp_dswiglu_f8, gemm_pp_f8, gemm_pp_rope_f8, gemm_pp_swiglu_f8,
+                   pp_f8_supported, wgrad, wgrad_supported)
 
 E4M3, E5M2 = 0, 1
 FMAX = {E4M3: 448.0, E5M2: 57344.0}
@@ -39,16 +40,30 @@ TORCH_DT = {E4M3: torch.float8_e4m3fn, E5M2: torch.float8_e5m2}
 
 AMAX_PARTS = 64
 _FUSED = {"enabled": True}
-# hipBLASLt stays the default: our kernel reaches 0.95x of its fp8 GEMMs per shape and costs 2.7 %
-# of the --fp8 step (profiles/r2_fp8_gemm_ab.md)
-_GEMM = {"backend": "hipblaslt"}
+# "pp" (default): the ping-pong kernel on fp8 operands (csrc/gemm_pp.hip F8, 16x16x128 f8f6f4 MFMA), which
+# also carries the fused RoPE / SwiGLU epilogues; "hip": the round-2 one-wave-per-SIMD fp8 kernel
+# (csrc/gemm_f8.hip); "hipblaslt": torch._scaled_mm.  Shapes the own kernels do not take fall back to
+# torch._scaled_mm.
+_GEMM = {"backend": "pp"}
+# fp8 projections with their fused epilogues on the own fp8 GEMM: q|k|v + RoPE, gate|up + SwiGLU and the
+# down input gradient + SwiGLU backward (backend "pp" only)
+_EPI = {"enabled": True}
 
 
 def set_fp8_gemm(backend: str) -> None:
-    """fp8 forward / input-gradient GEMMs on our MFMA kernel ("hip") or hipBLASLt ("hipblaslt", default)."""
-    if backend not in ("hip", "hipblaslt"):
+    """fp8 forward / input-gradient GEMMs: "pp" (default), "hip" or "hipblaslt"."""
+    if backend not in ("pp", "hip", "hipblaslt"):
         raise ValueError(backend)
     _GEMM["backend"] = backend
+
+
+def set_fp8_fused_epilogues(enabled: bool) -> None:
+    """RoPE / SwiGLU fused into the fp8 GEMMs (default on; needs the "pp" backend)."""
+    _EPI["enabled"] = bool(enabled)
+
+
+def fp8_fused_epilogues() -> bool:
+    return _EPI["enabled"] and _GEMM["backend"] == "pp"
 
 
 def fp8_gemm_backend() -> str:
@@ -57,6 +72,8 @@ def fp8_gemm_backend() -> str:
 
 def mm8(a8: torch.Tensor, b8: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) -> torch.Tensor:
     """bf16 sa * sb * a8 . b8^T (a8 [M, K], b8 [N, K] fp8)."""
+    if _GEMM["backend"] == "pp" and pp_f8_supported(a8, b8):
+        return gemm_pp_f8(a8, b8, sa, sb)
     if _GEMM["backend"] == "hip" and f8_nt_supported(a8, b8):
         return gemm_nt_f8(a8, b8, sa, sb)
     return torch._scaled_mm(a8, b8.t(), sa, sb, out_dtype=torch.bfloat16)
@@ -287,6 +304,82 @@ class Fp8LinearFn(torch.autograd.Function):
         return dx, None, None, None, None, None, None, None, None
 
 
+def _wgrad_bf16(gw, dy, x):
+    if gw is None:
+        return
+    if wgrad_supported(gw, dy, x):
+        wgrad(gw, dy, x)
+    else:
+        gw.add_(torch.mm(dy.t(), x).float())
+
+
+def _dy8(r: Fp8Recipe, k: int, dy: torch.Tensor) -> torch.Tensor:
+    dy8 = r.take_stashed(k, dy)  # written by a fused producer (RMSNorm backward)
+    return dy8 if dy8 is not None else r.quantize(dy, k, E5M2)
+
+
+class Fp8RopeFn(torch.autograd.Function):
+    """fp8 q|k|v projection with RoPE in the epilogue of the own fp8 GEMM (bf16 output, rotated q|k).
+    The attention backward returns the gradient of the UN-rotated projection, so the backward is the
+    plain fp8 projection backward (e5m2 dy x e4m3 W^T) plus the bf16 weight gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, gw, wq: "Fp8Weight", recipe: Fp8Recipe, kx: int, kdy: int, x8, cos, sin, T: int, hd: int,
+                rope_cols: int):
+        if x8 is None or x8.shape != x.shape:
+            x8 = recipe.quantize(x, kx, E4M3)
+        y = gemm_pp_rope_f8(x8, wq.w8, recipe.inv[kx:kx + 1], wq.inv, cos, sin, T, hd, rope_cols)
+        ctx.save_for_backward(x)
+        ctx.gw, ctx.wq, ctx.recipe, ctx.kdy = gw, wq, recipe, kdy
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        r, k = ctx.recipe, ctx.kdy
+        dx = mm8(_dy8(r, k, dy), ctx.wq.wT8, r.inv[k:k + 1], ctx.wq.inv)
+        _wgrad_bf16(ctx.gw, dy, x)
+        return (dx,) + (None,) * 12
+
+
+class Fp8MLPFn(torch.autograd.Function):
+    """The SwiGLU MLP with every projection in fp8 and both activation passes fused into the own fp8 GEMMs:
+
+      forward   gu, act = [e4m3 gate|up GEMM + SwiGLU epilogue](y8)
+                m       = act8 . W_down8^T            (act8: one cast of act, slot down.x)
+      backward  dgu     = [e5m2 down dgrad GEMM + SwiGLU-backward epilogue](dm8, W_down8^T copy, gu)
+                dy      = dgu8 . W_gu8               (dgu8: one cast of dgu, slot gu.dy)
+                gW_down += dm^T act, gW_gu += dgu^T y (bf16 weight-gradient kernel)"""
+
+    @staticmethod
+    def forward(ctx, y, w_gu, w_dn, gw_gu, gw_dn, wq_gu: "Fp8Weight", wq_dn: "Fp8Weight", recipe: Fp8Recipe,
+                ks, y8):
+        k_gx, k_gdy, k_dx, k_ddy = ks
+        if y8 is None or y8.shape != y.shape:
+            y8 = recipe.quantize(y, k_gx, E4M3)
+        gu, act = gemm_pp_swiglu_f8(y8, wq_gu.w8, recipe.inv[k_gx:k_gx + 1], wq_gu.inv)
+        act8 = recipe.quantize(act, k_dx, E4M3)
+        m = mm8(act8, wq_dn.w8, recipe.inv[k_dx:k_dx + 1], wq_dn.inv)
+        ctx.save_for_backward(y, gu, act)
+        ctx.gw, ctx.wq, ctx.recipe, ctx.ks = (gw_gu, gw_dn), (wq_gu, wq_dn), recipe, ks
+        return m
+
+    @staticmethod
+    def backward(ctx, dm):
+        y, gu, act = ctx.saved_tensors
+        gw_gu, gw_dn = ctx.gw
+        wq_gu, wq_dn = ctx.wq
+        r = ctx.recipe
+        _, k_gdy, _, k_ddy = ctx.ks
+        dm = dm.contiguous()
+        dgu = gemm_pp_dswiglu_f8(_dy8(r, k_ddy, dm), wq_dn.wT8, r.inv[k_ddy:k_ddy + 1], wq_dn.inv, gu)
+        _wgrad_bf16(gw_dn, dm, act)
+        dy = mm8(r.quantize(dgu, k_gdy, E5M2), wq_gu.wT8, r.inv[k_gdy:k_gdy + 1], wq_gu.inv)
+        _wgrad_bf16(gw_gu, dgu, y)
+        return (dy,) + (None,) * 9
+
+
 class Fp8Linears:
     """Per-model fp8 state: one recipe, one (x, dy) slot pair and one weight cache per projection."""
 
@@ -313,6 +406,29 @@ class Fp8Linears:
         if self.wgrad_fp8:
             return None
         return self.recipe.target(self._slots(key)[1], E5M2)
+
+    def rope_ok(self, x: torch.Tensor, w: torch.Tensor, hd: int, rope_cols: int) -> bool:
+        """Can the q|k|v projection run as fp8 GEMM + fused RoPE (own kernel)."""
+        return (fp8_fused_epilogues() and not self.wgrad_fp8 and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
+                and x.shape[1] % 128 == 0 and w.shape[0] % 8 == 0 and hd in (32, 64) and rope_cols % 64 == 0)
+
+    def rope(self, key: str, x, w, gw, version: int, x8, cos, sin, T: int, hd: int, rope_cols: int):
+        kx, kdy = self._slots(key)
+        wq = self.weights[key].get(w, version)
+        return Fp8RopeFn.apply(x, w, gw, wq, self.recipe, kx, kdy, x8, cos, sin, int(T), int(hd), int(rope_cols))
+
+    def mlp_ok(self, y: torch.Tensor, w_gu: torch.Tensor, w_dn: torch.Tensor) -> bool:
+        """Can the MLP run as fp8 GEMMs with the fused SwiGLU forward / backward epilogues."""
+        F = w_gu.shape[0] // 2
+        return (fp8_fused_epilogues() and not self.wgrad_fp8 and y.is_cuda and y.dim() == 2 and y.stride(1) == 1
+                and y.shape[1] % 128 == 0 and F % 128 == 0 and w_dn.shape[1] == F and w_dn.shape[0] % 128 == 0)
+
+    def mlp(self, kgu: str, kdn: str, y, w_gu, w_dn, gw_gu, gw_dn, version: int, y8=None):
+        k_gx, k_gdy = self._slots(kgu)
+        k_dx, k_ddy = self._slots(kdn)
+        wq_gu = self.weights[kgu].get(w_gu, version)
+        wq_dn = self.weights[kdn].get(w_dn, version)
+        return Fp8MLPFn.apply(y, w_gu, w_dn, gw_gu, gw_dn, wq_gu, wq_dn, self.recipe, (k_gx, k_gdy, k_dx, k_ddy), y8)
 
     def __call__(self, key: str, x: torch.Tensor, w: torch.Tensor, gw: Optional[torch.Tensor], version: int,
                  x8: Optional[torch.Tensor] = None):

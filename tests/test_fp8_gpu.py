@@ -68,9 +68,10 @@ def test_fp8_weight_current_scaling(shape):
     assert wq.get(w, version=0) is wq and wq.version == 0
 
 
-@pytest.fixture(params=["hipblaslt", "hip"])
+@pytest.fixture(params=["pp", "hipblaslt", "hip"])
 def fp8_gemm(request):
-    """Both fp8 GEMM backends: hipBLASLt (default) and the own MFMA kernel (csrc/gemm.hip)."""
+    """The fp8 GEMM backends: the own ping-pong kernel (default; with the fused RoPE / SwiGLU epilogues
+    in the model), hipBLASLt, and the round-2 own kernel (csrc/gemm_f8.hip)."""
     old = fp8.fp8_gemm_backend()
     fp8.set_fp8_gemm(request.param)
     yield request.param
@@ -243,3 +244,47 @@ def test_fused_quant_training_matches_separate_casts():
     l1, p1 = run(True)
     assert (l1 - l0).abs().max().item() < 2e-3, (l0, l1)
     assert ((p1 - p0).norm() / p0.norm()).item() < 1e-3
+
+
+def test_fp8_fused_epilogues_track_unfused():
+    """fp8 projections with RoPE / SwiGLU fused into the own fp8 GEMMs (default) train like the same fp8
+    model with separate RoPE / SwiGLU passes, and actually take the fused path."""
+    cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=768, num_attention_heads=4,
+                                     num_key_value_heads=4, num_hidden_layers=2, vocab_size=512))
+    ids = torch.randint(0, 512, (8, 256), device="cuda")
+    losses = {}
+    try:
+        for fused in (False, True):
+            fp8.set_fp8_fused_epilogues(fused)
+            m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16, fp8=True).init_weights(5)
+            calls = {"rope": 0, "mlp": 0}
+            orig_rope, orig_mlp = fp8.Fp8RopeFn.apply, fp8.Fp8MLPFn.apply
+
+            def rope_apply(*a, _o=orig_rope):
+                calls["rope"] += 1
+                return _o(*a)
+
+            def mlp_apply(*a, _o=orig_mlp):
+                calls["mlp"] += 1
+                return _o(*a)
+
+            fp8.Fp8RopeFn.apply, fp8.Fp8MLPFn.apply = rope_apply, mlp_apply
+            try:
+                opt = FlatAdamW(m.store, lr=3e-3)
+                ls = []
+                for _ in range(20):
+                    out = m(ids, labels=ids)
+                    out.loss.backward()
+                    opt.step()
+                    m.fp8.recipe.update()
+                    m.store.zero_grad()
+                    ls.append(out.loss.item())
+            finally:
+                fp8.Fp8RopeFn.apply, fp8.Fp8MLPFn.apply = orig_rope, orig_mlp
+            assert (calls["rope"] > 0) == fused and (calls["mlp"] > 0) == fused, calls
+            losses[fused] = ls
+    finally:
+        fp8.set_fp8_fused_epilogues(True)
+    u, f = losses[False], losses[True]
+    assert f[-1] < 0.5 * f[0], f
+    assert abs(f[-1] - u[-1]) < 0.1 * u[0], (u[-1], f[-1])
