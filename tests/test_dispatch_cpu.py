@@ -10,14 +10,23 @@ from nanodiloco_amd.ops import gemm as G
 
 def test_fp8_gemm_backend_switch():
     old = fp8.fp8_gemm_backend()
-    assert old == "hipblaslt"  # measured default (profiles/r2_fp8_gemm_ab.md)
+    assert old == "pp"  # the own fp8 ping-pong kernel with fused epilogues (profiles/r4_fp8_pp.md)
+    assert fp8.fp8_fused_epilogues()
     try:
         fp8.set_fp8_gemm("hip")
         assert fp8.fp8_gemm_backend() == "hip"
+        assert not fp8.fp8_fused_epilogues()  # the fused fp8 epilogues live in the pp kernel only
+        fp8.set_fp8_gemm("hipblaslt")
+        assert fp8.fp8_gemm_backend() == "hipblaslt"
         with pytest.raises(ValueError):
             fp8.set_fp8_gemm("cublas")
     finally:
         fp8.set_fp8_gemm(old)
+
+
+def test_pp_f8_supported_gate_on_cpu():
+    a = torch.zeros(256, 256, dtype=torch.float8_e4m3fn)
+    assert not G.pp_f8_supported(a, a)  # CPU tensors never take the HIP kernel
 
 
 def test_f8_nt_supported_gate_on_cpu_and_shapes():
