@@ -843,6 +843,179 @@ __global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restri
   }
 }
 
+// =====================================================================================================
+// fp8 weight-gradient kernel (round 4): C (+)= sa sb dY8^T X8 with dY8 [K, M] (e5m2 or e4m3) and X8 [K, N]
+// (e4m3) as the producers wrote them (token-major, no transposed copies).  wgrad_pp_kernel's ping-pong
+// structure with the K-tile doubled to 128 tokens, so the LDS image (128 k-rows x 128 B per half-tile), the
+// DMA pieces (8 rows x 128 B) and the per-K-tile instruction counts stay those of the bf16 kernel while
+// each K-tile carries twice the work: 48 ds_read_b64_tr_b8 per wave (4 per fragment: 8 k-rows of 16
+// columns each, the lane's 32 K bytes) and 32 v_mfma_scale_f32_16x16x128_f8f6f4 (twice the bf16 rate).
+// LDS chunk swizzle f(r) = ((r >> 1) & 3) ^ (((r >> 5) & 1) << 2): the two 16-lane groups of a 32-lane half
+// read rows 32 apart, 8 rows x 16 B each -> 16 distinct 4-bank sets (conflict-free).
+namespace {
+constexpr uint32_t W8_HALF_B = 128 * 128;      // [128 k][128 cols] bytes
+constexpr uint32_t W8_BUF_B = 4 * W8_HALF_B;   // A0 A1 B0 B1 = 64 KiB
+typedef int w8v2 __attribute__((ext_vector_type(2)));
+typedef int w8v8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int w8_swz(int r) { return ((r >> 1) & 3) ^ (((r >> 5) & 1) << 2); }
+// 16x16x128 operand, the column on the lane: lane l -> column c0 + (l & 15), k = 32 (l >> 4) + 0 .. 31
+__device__ __forceinline__ w8v8 w8_frag(const char* half, int c0, int lane) {
+  const int gq = lane >> 4, j = lane & 15, q = j >> 1, p = j & 1;
+  const int ch = c0 >> 4;  // c0 % 16 == 0
+  w8v8 r;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int row = 32 * gq + 8 * t + q;
+    const char* a = half + row * 128 + ((ch ^ w8_swz(row)) << 4) + 8 * p;
+    const w8v2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((w8v2 __attribute__((address_space(3)))*)(a));
+    r[2 * t] = v[0];
+    r[2 * t + 1] = v[1];
+  }
+  return r;
+}
+}  // namespace
+
+// FA: dY's format (0 e4m3, 1 e5m2); X is e4m3
+template <int FA>
+__global__ void __launch_bounds__(512, 1) wgrad8_pp_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                           float* __restrict__ C, float* __restrict__ slab, int M, int N,
+                                                           int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
+                                                           int kchunk, const float* __restrict__ sa,
+                                                           const float* __restrict__ sb) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem_bf[];
+  char* smem = reinterpret_cast<char*>(smem_bf);
+  const int tn_count = (N + 255) / 256;
+  const int tiles = ((M + 255) / 256) * tn_count;
+  const int id = xcd_remap(blockIdx.x, tiles * S);
+  const int split = id / tiles, tile = id % tiles;
+  const int m0 = (tile / tn_count) * 256, n0 = (tile % tn_count) * 256;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int nk = (kend - kbeg) / 128;  // host: K % 128 == 0, kchunk % 128 == 0, every split non-empty
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = w >> 2, wn = w & 3;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  const float sc = sa[0] * sb[0];
+
+  // DMA piece q of this wave = half-tile k-rows 8 j .. 8 j + 7 (j = wn + 4 q); lane -> row 8 j + lane / 8,
+  // physical chunk lane & 7 <- logical chunk (lane & 7) ^ f(row)
+  const int64_t ld = g == 0 ? ldb : lda;
+  uint32_t voff[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = 8 * (wn + 4 * q) + (lane >> 3);
+    voff[q] = (uint32_t)((int64_t)row * ld + (((lane & 7) ^ w8_swz(row)) << 4));
+  }
+  auto stage = [&](int kt, int h) __attribute__((always_inline)) {
+    const int64_t e0 = (int64_t)(kbeg + 128 * kt) * ld + (g == 0 ? n0 : m0) + 128 * h;
+    const uint32_t dst = lds0 + (uint32_t)(kt & 1) * W8_BUF_B + (uint32_t)(g == 0 ? 2 + h : h) * W8_HALF_B +
+                         (uint32_t)wn * 1024u;
+    if (g == 0 ? n0 + 128 * h + 128 <= N : m0 + 128 * h + 128 <= M) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wpp_gdma((g == 0 ? B : A) + e0, voff[q], dst + (uint32_t)q * 4096u);
+    } else {
+      const auto r = wpp_rsrc((g == 0 ? B : A) + e0, (int64_t)K * ld - e0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wpp_dma(r, voff[q], dst + (uint32_t)q * 4096u);
+    }
+  };
+  w8v8 fa[8], fb[4];
+  auto load_frags = [&](int kt) __attribute__((always_inline)) {
+    const char* base = smem + (kt & 1) * W8_BUF_B;
+    const char* ah = base + g * W8_HALF_B;
+    const char* bh = base + (2 + (wn >> 1)) * W8_HALF_B;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) fb[b] = w8_frag(bh, (wn & 1) * 64 + 16 * b, lane);
+#pragma unroll
+    for (int a = 0; a < 8; ++a) fa[a] = w8_frag(ah, 16 * a, lane);
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (g == 0) {
+    stage(0, 0);
+    stage(0, 1);
+  } else {
+    stage(0, 0);
+    stage(0, 1);
+    if (nk > 1) stage(1, 0);
+  }
+  wpp_vm<0>();
+  wpp_bar();
+  if (g == 1) wpp_bar();
+  for (int s = 0; s < nk; ++s) {
+    const bool more1 = s + 1 < nk, more2 = s + 2 < nk;
+    // ================= LOAD(s)
+    if (g == 0) {
+      if (more1) {
+        stage(s + 1, 0);
+        stage(s + 1, 1);
+      }
+    } else {
+      if (more1) stage(s + 1, 1);  // A1(s + 1)
+      if (more2) stage(s + 2, 0);  // A0(s + 2)
+    }
+    load_frags(s);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (g == 1) wpp_vmn((more1 ? 4 : 0) + (more2 ? 4 : 0));  // A0(s + 1) landed
+    wpp_bar();
+    // ================= COMPUTE(s)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[a], fb[b], acc[a][b], FA, 0, 0, 0x7f7f7f7f, 0,
+                                                                     0x7f7f7f7f);
+    __builtin_amdgcn_s_setprio(0);
+    if (g == 0) wpp_vm<0>();            // B(s + 1) landed
+    else wpp_vmn(more2 ? 4 : 0);        // A1(s + 1) landed
+    wpp_bar();
+  }
+  // epilogue: wgrad_pp_kernel's (acc[a][b] lane l reg r = C[m0 + 128 g + 16 a + 4 (l >> 4) + r]
+  // [n0 + 64 wn + 16 b + (l & 15)]), dequantised by sc
+  if (g == 0) wpp_bar();
+  float* out = S == 1 ? C : slab + (int64_t)split * M * N;
+  const int64_t ldo = S == 1 ? ldc : N;
+  float* reg = reinterpret_cast<float*>(smem) + w * (64 * 64);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * a + 4 * (lane >> 4) + r, col = 16 * b + (lane & 15);
+          reg[row * 64 + (((col >> 2) ^ (row & 15)) << 2) + (col & 3)] = acc[4 * half + a][b][r] * sc;
+        }
+    asm volatile("" ::: "memory");
+    const int c4 = lane & 15;
+    const int n = n0 + wn * 64 + 4 * c4;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = 4 * i + (lane >> 4);
+      const float4 v = *reinterpret_cast<const float4*>(reg + row * 64 + ((c4 ^ (row & 15)) << 2));
+      const int m = m0 + g * 128 + 64 * half + row;
+      if (m < M && n < N) {
+        float4* p = reinterpret_cast<float4*>(out + (int64_t)m * ldo + n);
+        if (S == 1) {
+          float4 c = *p;
+          c.x += v.x; c.y += v.y; c.z += v.z; c.w += v.w;
+          *p = c;
+        } else {
+          *p = v;
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+  }
+}
+
 static int splits_for(int tiles, int K, int bk, int target) {
   int S = target / tiles;
   if (S < 1) S = 1;
@@ -976,6 +1149,40 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
     hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * S), dim3(256), 0, s, (const bf16_t*)A, (const bf16_t*)B, C, slab, M,
                        N, K, lda, ldb, ldc, S, kchunk);
   }
+  if (S > 1) {
+    int64_t blocks = ((int64_t)M * N / 4 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, slab, C, M, N, ldc, S);
+  }
+  ND_LAUNCH_CHECK();
+}
+
+// fp8 weight gradient: C[M, N] (fp32) += sa sb A^T B with A = dY8 [K, M] (lda bytes; fa 0 e4m3, 1 e5m2),
+// B = X8 [K, N] (ldb bytes, e4m3).  K % 128 == 0, M, N % 16 == 0, lda / ldb % 16 == 0.  Slab workspace as
+// nd_wgrad (nd_wgrad_splits(M, N, K) planes).
+ND_API int nd_wgrad_f8(const void* A, const void* B, float* C, float* slab, int M, int N, int K, int64_t lda,
+                       int64_t ldb, int64_t ldc, const float* sa, const float* sb, int fa, hipStream_t s) {
+  if (M % 16 || N % 16 || lda % 16 || ldb % 16 || ldc % 4 || K % 128 || K <= 0 || M < 256 || N < 256 || !sa || !sb ||
+      (fa != 0 && fa != 1) || (int64_t)128 * (lda > ldb ? lda : ldb) >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  int S;
+  plan(M, N, K, &S);
+  if (S > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
+  const int kchunk = fit_kchunk(K, &S, 128);
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const size_t lds = 2 * (size_t)W8_BUF_B;  // 128 KiB
+  static const hipError_t attr =
+      (hipError_t)(hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad8_pp_kernel<0>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) |
+                   hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad8_pp_kernel<1>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  if (attr != hipSuccess) return (int)attr;
+  if (fa == 0)
+    hipLaunchKernelGGL(wgrad8_pp_kernel<0>, dim3(tiles * S), dim3(512), lds, s, (const uint8_t*)A, (const uint8_t*)B, C,
+                       slab, M, N, K, lda, ldb, ldc, S, kchunk, sa, sb);
+  else
+    hipLaunchKernelGGL(wgrad8_pp_kernel<1>, dim3(tiles * S), dim3(512), lds, s, (const uint8_t*)A, (const uint8_t*)B, C,
+                       slab, M, N, K, lda, ldb, ldc, S, kchunk, sa, sb);
   if (S > 1) {
     int64_t blocks = ((int64_t)M * N / 4 + 255) / 256;
     if (blocks > 4096) blocks = 4096;

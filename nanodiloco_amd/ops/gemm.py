@@ -250,6 +250,31 @@ def wgrad(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
                           gw.stride(0), _ext.stream_ptr(gw.device)), "nd_wgrad")
 
 
+def wgrad_f8_supported(gw: torch.Tensor, dy8: torch.Tensor, x8: torch.Tensor) -> bool:
+    """Can ``wgrad_f8`` run: fp8 token-major operands (dy e4m3 / e5m2, x e4m3), tokens % 128, M, N >= 256."""
+    return (gw.is_cuda and _ext.get_backend() != "torch" and gw.dtype == torch.float32 and dy8.dim() == 2
+            and x8.dim() == 2 and dy8.dtype in _F8_FMT and x8.dtype == torch.float8_e4m3fn
+            and dy8.shape[0] == x8.shape[0] and dy8.shape[0] % 128 == 0 and dy8.shape[1] % 16 == 0
+            and x8.shape[1] % 16 == 0 and dy8.shape[1] >= 256 and x8.shape[1] >= 256 and dy8.stride(1) == 1
+            and x8.stride(1) == 1 and gw.stride(1) == 1 and dy8.stride(0) % 16 == 0 and x8.stride(0) % 16 == 0
+            and gw.stride(0) % 4 == 0 and dy8.data_ptr() % 16 == 0 and x8.data_ptr() % 16 == 0)
+
+
+def wgrad_f8(gw: torch.Tensor, dy8: torch.Tensor, x8: torch.Tensor, s_dy: torch.Tensor, s_x: torch.Tensor) -> None:
+    """gw[M, N] (fp32) += s_dy * s_x * dy8[K, M]^T . x8[K, N]: the fp8 weight gradient straight from the
+    token-major fp8 operands the forward / input-gradient GEMMs already use (csrc/gemm_wgrad.hip
+    wgrad8_pp_kernel: transposing ds_read_b64_tr_b8 fragments, 16x16x128 f8f6f4 MFMA)."""
+    K, M = dy8.shape
+    N = x8.shape[1]
+    assert x8.shape[0] == K and tuple(gw.shape) == (M, N)
+    L = _ext.lib()
+    S = L.nd_wgrad_splits(M, N, K)
+    ws = _workspace(gw.device, S * M * N) if S > 1 else None
+    _ext.check(L.nd_wgrad_f8(_ext.ptr(dy8), _ext.ptr(x8), _ext.ptr(gw), _ext.ptr(ws), M, N, K, dy8.stride(0),
+                             x8.stride(0), gw.stride(0), _ext.ptr(s_dy), _ext.ptr(s_x), _F8_FMT[dy8.dtype],
+                             _ext.stream_ptr(gw.device)), "nd_wgrad_f8")
+
+
 def set_w128_ablation(v: int) -> int:
     """Ablation builds of the w128 kernel (profiling only -- WRONG results): 1 no LDS-DMA, 2 no fragment
     reads, 4 no barriers, 8 no epilogue stores, 16 no vmcnt waits in the loop, 31 all; 0 = the kernel."""

@@ -89,6 +89,16 @@ def main():
     cases.append(("down dgrad+dswiglu", 2.0 * M * F * d,
                   {"pp f8": lambda: G.gemm_pp_dswiglu_f8(dy8, wdt8, sdy, sdt, gu, dgu),
                    "pp bf16": lambda: G.gemm_pp_dswiglu(xb, wdtb, gu, dgu)}))
+    # weight gradients: bf16 wgrad_pp vs fp8 wgrad8_pp on the same token-major operands
+    for name, m_, n_ in (("wgrad qkv", 3 * d, d), ("wgrad o", d, d), ("wgrad gate|up", 2 * F, d), ("wgrad down", d, F)):
+        dyf, xf = torch.randn(M, m_, device="cuda"), torch.randn(M, n_, device="cuda")
+        dy8_, sdy_ = q8(dyf, E5)
+        x8_, sx_ = q8(xf, E4)
+        dyb, xb_ = dyf.bfloat16(), xf.bfloat16()
+        gw = torch.zeros(m_, n_, device="cuda")
+        cases.append((name, 2.0 * M * m_ * n_,
+                      {"wgrad f8": (lambda g=gw, a_=dy8_, b_=x8_, s1=sdy_, s2=sx_: G.wgrad_f8(g, a_, b_, s1, s2)),
+                       "wgrad bf16": (lambda g=gw, a_=dyb, b_=xb_: G.wgrad(g, a_, b_))}))
     res = {}
     for _ in range(a.rounds):
         for name, fl, arms in cases:

@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 4, session 11: ds_read_b64_tr_b8 semantics probe, then the fp8 weight-gradient kernel: numerics and
+# timing vs the bf16 one (plus the fp8 projection GEMMs again)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${SESSION:-r4s}
+mkdir -p $O
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 200 python -u -m pytest tests/test_probe_gpu.py -x -q -s --timeout 120 --timeout-method thread > $O/probe.log 2>&1
+rc=$?; tail -5 $O/probe.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u -m pytest tests/test_gemm_pp_f8_gpu.py -x -q --timeout 120 --timeout-method thread > $O/test.log 2>&1
+rc=$?; tail -15 $O/test.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u scripts/gemm_pp_f8_bench.py --rounds 5 > $O/bench.log 2>&1
+rc=$?; cat $O/bench.log; exit $rc

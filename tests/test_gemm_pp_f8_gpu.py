@@ -133,3 +133,36 @@ def test_gemm_pp_f8_deterministic():
     c1 = G.gemm_pp_f8(a8, b8, sa, sb)
     c2 = G.gemm_pp_f8(a8, b8, sa, sb)
     assert torch.equal(c1, c2)
+
+
+# ---------------------------------------------------------------- fp8 weight gradient (wgrad8_pp_kernel)
+WG_SHAPES = [(256, 256, 128), (1024, 1024, 4096), (3072, 1024, 8192), (1024, 2688, 2048), (5376, 1024, 4096),
+             (1000 // 16 * 16, 528, 1024), (2688, 1024, 384), (256, 32000 // 16 * 16, 256)]
+
+
+@pytest.mark.parametrize("ddt", [E5, E4], ids=["e5m2", "e4m3"])
+@pytest.mark.parametrize("M,N,K", WG_SHAPES)
+def test_wgrad_f8(M, N, K, ddt):
+    dy8, sdy = q8(torch.randn(K, M, device=DEV), ddt)
+    x8, sx = q8(torch.randn(K, N, device=DEV), E4)
+    gw0 = torch.randn(M, N, device=DEV)
+    gw = gw0.clone()
+    G.wgrad_f8(gw, dy8, x8, sdy, sx)
+    ref = gw0 + (dy8.float().t() @ x8.float()) * (sdy * sx)
+    assert rel(gw - gw0, ref - gw0) < 2e-3
+    assert maxrel(gw - gw0, ref - gw0) < 1e-2
+
+
+def test_wgrad_f8_strided_and_deterministic():
+    K, M, N = 2048, 1024, 768
+    dyf, sdy = q8(torch.randn(K, M + 64, device=DEV), E5)
+    xf, sx = q8(torch.randn(K, N + 32, device=DEV), E4)
+    dy8, x8 = dyf[:, 64:], xf[:, :N]
+    out = []
+    for _ in range(2):
+        gw = torch.zeros(M, N, device=DEV)
+        G.wgrad_f8(gw, dy8, x8, sdy, sx)
+        out.append(gw)
+    ref = (dy8.float().t() @ x8.float()) * (sdy * sx)
+    assert rel(out[0], ref) < 2e-3
+    assert torch.equal(out[0], out[1])
