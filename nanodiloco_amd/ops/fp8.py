@@ -1,15 +1,17 @@
 """fp8 inner step (BASELINE config 5): OCP fp8 GEMMs for the decoder projections on gfx950.
 
 Recipe (per-tensor scaling, the common "delayed scaling" scheme):
-* forward  ``y = x @ W^T`` with x, W in e4m3 -> hipBLASLt (``torch._scaled_mm``, default) or our fp8
-  MFMA GEMM (``gemm.gemm_nt_f8``, ``v_mfma_scale_f32_32x32x64_f8f6f4``; ``set_fp8_gemm("hip")``), bf16 out;
-* dgrad    ``dx = dy @ W`` with dy in e5m2 (range for gradients), W^T in e4m3;
-* wgrad    ``dW = dy^T x`` as an fp8 GEMM too (e5m2 x e4m3, fp32 out, added into the flat fp32 grad
-  buffer); its K-major operands dy^T / x^T come from ``nd_fp8_cast_t``, which writes the fp8 tensor
-  AND its transpose in one pass -- the forward saves x^T in fp8 (half the bytes of bf16 x).
-  Off by default (``wgrad_fp8=False`` = bf16 ``nd_wgrad``): on the Llama-150M shapes hipBLASLt's fp8
-  kernel for this K = 32768 reduction ran at ~215 us vs ~236 us for our bf16 kernel, which the
-  transposing casts (65-115 us) more than eat (profiles/r1_bench150m_fp8_kernel_stats_v2.md);
+* forward  ``y = x @ W^T`` with x, W in e4m3 on the own ping-pong GEMM in its fp8 form (``gemm.gemm_pp_f8``,
+  csrc/gemm_pp.hip F8: one ``v_mfma_scale_f32_16x16x128_f8f6f4`` per 128-deep K-tile of the same LDS image
+  as the bf16 kernel; default ``set_fp8_gemm("pp")``), bf16 out.  The q|k|v projection keeps RoPE and the
+  MLP keeps SwiGLU / its backward in that GEMM's epilogues (``Fp8RopeFn``, ``Fp8MLPFn``; on the dequantised
+  fp32 accumulator).  ``"hipblaslt"`` (``torch._scaled_mm``) and ``"hip"`` (the round-2 kernel,
+  csrc/gemm_f8.hip) are the A/B alternatives; they run the RoPE / SwiGLU passes separately;
+* dgrad    ``dx = dy @ W`` with dy in e5m2 (range for gradients), W^T in e4m3, same kernels;
+* wgrad    ``dW = dy^T x``: bf16 ``nd_wgrad`` by default; with ``wgrad_fp8`` the own fp8 kernel
+  (``gemm.wgrad_f8``, csrc/gemm_wgrad.hip wgrad8_pp_kernel) straight from the token-major fp8 operands
+  the other two GEMMs already use -- ``ds_read_b64_tr_b8`` transposes them on the way out of LDS, so no
+  transposed copies are written, and the forward keeps x8 (half the bytes of x) for the backward;
 * activations / gradients are quantised by ``nd_fp8_cast`` (one pass: scale, saturate, convert,
   and record amax) with a scale derived from the amax history of previous steps (``Fp8Recipe``;
   device-side, no host sync); the very first use of a tensor role is scaled from its current amax;
@@ -21,7 +23,8 @@ Recipe (per-tensor scaling, the common "delayed scaling" scheme):
   SwiGLU backward -> dy of gate|up, RMSNorm backward -> dy of o and down.  (The attention
   epilogues stay plain: their fused variants cost occupancy -- measured -2.6 % end to end.)  The backward side
   reaches the consuming ``Fp8LinearFn.backward`` through ``Fp8Recipe.stash`` (keyed by slot, checked
-  against the gradient tensor's storage).  Bitwise the separate cast over the bf16 tensor.
+  against the gradient tensor's storage).  Bitwise the separate cast over the bf16 tensor.  With the
+  fused-epilogue MLP the SwiGLU outputs come from the GEMM epilogue and act / d(gate|up) get one cast each.
 """
 from __future__ import annotations
 
@@ -31,7 +34,7 @@ import torch
 
 from . import _ext
 from .gemm import (f8_nt_supported, gemm_nt_f8, gemm_pp_dswiglu_f8, gemm_pp_f8, gemm_pp_rope_f8, gemm_pp_swiglu_f8,
-                   pp_f8_supported, wgrad, wgrad_supported)
+                   pp_f8_supported, wgrad, wgrad_f8, wgrad_f8_supported, wgrad_supported)
 
 E4M3, E5M2 = 0, 1
 FMAX = {E4M3: 448.0, E5M2: 57344.0}
@@ -268,13 +271,10 @@ class Fp8Weight:
 class Fp8LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, gw, wq: Fp8Weight, recipe: Fp8Recipe, kx: int, kdy: int, wgrad_fp8: bool, x8=None):
-        if wgrad_fp8:
-            x8, x8t = recipe.quantize_t(x, kx, E4M3)
-            ctx.save_for_backward(x8t)
-        else:
-            if x8 is None or x8.shape != x.shape:
-                x8 = recipe.quantize(x, kx, E4M3)
-            ctx.save_for_backward(x)
+        if x8 is None or x8.shape != x.shape:
+            x8 = recipe.quantize(x, kx, E4M3)
+        # fp8 weight gradient: keep x8 (half the bytes of x) for dW = dy8^T x8
+        ctx.save_for_backward(x8 if wgrad_fp8 else x)
         inv_x = recipe.inv[kx:kx + 1]
         y = mm8(x8, wq.w8, inv_x, wq.inv)
         ctx.gw, ctx.wq, ctx.recipe, ctx.kdy, ctx.inv_x, ctx.wgrad_fp8 = gw, wq, recipe, kdy, inv_x, wgrad_fp8
@@ -285,22 +285,13 @@ class Fp8LinearFn(torch.autograd.Function):
         (xs,) = ctx.saved_tensors
         dy = dy.contiguous()
         r, k = ctx.recipe, ctx.kdy
-        if ctx.wgrad_fp8:
-            dy8, dy8t = r.quantize_t(dy, k, E5M2)
-        else:
-            dy8 = r.take_stashed(k, dy)  # written by the fused producer (SwiGLU / RMSNorm backward)
-            if dy8 is None:
-                dy8 = r.quantize(dy, k, E5M2)
+        dy8 = _dy8(r, k, dy)
         inv_dy = r.inv[k:k + 1]
         dx = mm8(dy8, ctx.wq.wT8, inv_dy, ctx.wq.inv)
-        if ctx.gw is not None:
-            if ctx.wgrad_fp8:
-                # dW[out, in] = dy^T x : mat1 = dy^T (row-major), mat2 = x as column-major [T, in]
-                ctx.gw.add_(torch._scaled_mm(dy8t, xs.t(), inv_dy, ctx.inv_x, out_dtype=torch.float32))
-            elif wgrad_supported(ctx.gw, dy, xs):
-                wgrad(ctx.gw, dy, xs)
-            else:
-                ctx.gw.add_(torch.mm(dy.t(), xs).float())
+        if ctx.wgrad_fp8:
+            _wgrad_f8(ctx.gw, dy8, xs, inv_dy, ctx.inv_x, dy)
+        else:
+            _wgrad_bf16(ctx.gw, dy, xs)
         return dx, None, None, None, None, None, None, None, None
 
 
@@ -311,6 +302,17 @@ def _wgrad_bf16(gw, dy, x):
         wgrad(gw, dy, x)
     else:
         gw.add_(torch.mm(dy.t(), x).float())
+
+
+def _wgrad_f8(gw, dy8, x8, inv_dy, inv_x, dy):
+    """gw += dy^T x from the fp8 operands (own kernel, csrc/gemm_wgrad.hip wgrad8_pp_kernel); shapes it does
+    not take fall back to the bf16 kernel on the dequantised input."""
+    if gw is None:
+        return
+    if wgrad_f8_supported(gw, dy8, x8):
+        wgrad_f8(gw, dy8, x8, inv_dy, inv_x)
+    else:
+        _wgrad_bf16(gw, dy, (x8.float() * inv_x).to(dy.dtype))
 
 
 def _dy8(r: Fp8Recipe, k: int, dy: torch.Tensor) -> torch.Tensor:
@@ -325,22 +327,27 @@ class Fp8RopeFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, gw, wq: "Fp8Weight", recipe: Fp8Recipe, kx: int, kdy: int, x8, cos, sin, T: int, hd: int,
-                rope_cols: int):
+                rope_cols: int, wgrad_fp8: bool):
         if x8 is None or x8.shape != x.shape:
             x8 = recipe.quantize(x, kx, E4M3)
-        y = gemm_pp_rope_f8(x8, wq.w8, recipe.inv[kx:kx + 1], wq.inv, cos, sin, T, hd, rope_cols)
-        ctx.save_for_backward(x)
-        ctx.gw, ctx.wq, ctx.recipe, ctx.kdy = gw, wq, recipe, kdy
+        inv_x = recipe.inv[kx:kx + 1]
+        y = gemm_pp_rope_f8(x8, wq.w8, inv_x, wq.inv, cos, sin, T, hd, rope_cols)
+        ctx.save_for_backward(x8 if wgrad_fp8 else x)
+        ctx.gw, ctx.wq, ctx.recipe, ctx.kdy, ctx.inv_x, ctx.wgrad_fp8 = gw, wq, recipe, kdy, inv_x, wgrad_fp8
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        (x,) = ctx.saved_tensors
+        (xs,) = ctx.saved_tensors
         dy = dy.contiguous()
         r, k = ctx.recipe, ctx.kdy
-        dx = mm8(_dy8(r, k, dy), ctx.wq.wT8, r.inv[k:k + 1], ctx.wq.inv)
-        _wgrad_bf16(ctx.gw, dy, x)
-        return (dx,) + (None,) * 12
+        dy8 = _dy8(r, k, dy)
+        dx = mm8(dy8, ctx.wq.wT8, r.inv[k:k + 1], ctx.wq.inv)
+        if ctx.wgrad_fp8:
+            _wgrad_f8(ctx.gw, dy8, xs, r.inv[k:k + 1], ctx.inv_x, dy)
+        else:
+            _wgrad_bf16(ctx.gw, dy, xs)
+        return (dx,) + (None,) * 13
 
 
 class Fp8MLPFn(torch.autograd.Function):
@@ -354,30 +361,39 @@ class Fp8MLPFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, w_gu, w_dn, gw_gu, gw_dn, wq_gu: "Fp8Weight", wq_dn: "Fp8Weight", recipe: Fp8Recipe,
-                ks, y8):
+                ks, y8, wgrad_fp8: bool):
         k_gx, k_gdy, k_dx, k_ddy = ks
         if y8 is None or y8.shape != y.shape:
             y8 = recipe.quantize(y, k_gx, E4M3)
         gu, act = gemm_pp_swiglu_f8(y8, wq_gu.w8, recipe.inv[k_gx:k_gx + 1], wq_gu.inv)
         act8 = recipe.quantize(act, k_dx, E4M3)
         m = mm8(act8, wq_dn.w8, recipe.inv[k_dx:k_dx + 1], wq_dn.inv)
-        ctx.save_for_backward(y, gu, act)
-        ctx.gw, ctx.wq, ctx.recipe, ctx.ks = (gw_gu, gw_dn), (wq_gu, wq_dn), recipe, ks
+        # fp8 weight gradients keep the fp8 operands (y8, act8) instead of the bf16 ones
+        ctx.save_for_backward(y8 if wgrad_fp8 else y, gu, act8 if wgrad_fp8 else act)
+        ctx.gw, ctx.wq, ctx.recipe, ctx.ks, ctx.wgrad_fp8 = (gw_gu, gw_dn), (wq_gu, wq_dn), recipe, ks, wgrad_fp8
         return m
 
     @staticmethod
     def backward(ctx, dm):
-        y, gu, act = ctx.saved_tensors
+        ys, gu, acts = ctx.saved_tensors
         gw_gu, gw_dn = ctx.gw
         wq_gu, wq_dn = ctx.wq
         r = ctx.recipe
-        _, k_gdy, _, k_ddy = ctx.ks
+        k_gx, k_gdy, k_dx, k_ddy = ctx.ks
         dm = dm.contiguous()
-        dgu = gemm_pp_dswiglu_f8(_dy8(r, k_ddy, dm), wq_dn.wT8, r.inv[k_ddy:k_ddy + 1], wq_dn.inv, gu)
-        _wgrad_bf16(gw_dn, dm, act)
-        dy = mm8(r.quantize(dgu, k_gdy, E5M2), wq_gu.wT8, r.inv[k_gdy:k_gdy + 1], wq_gu.inv)
-        _wgrad_bf16(gw_gu, dgu, y)
-        return (dy,) + (None,) * 9
+        dm8 = _dy8(r, k_ddy, dm)
+        dgu = gemm_pp_dswiglu_f8(dm8, wq_dn.wT8, r.inv[k_ddy:k_ddy + 1], wq_dn.inv, gu)
+        dgu8 = r.quantize(dgu, k_gdy, E5M2)
+        if ctx.wgrad_fp8:
+            _wgrad_f8(gw_dn, dm8, acts, r.inv[k_ddy:k_ddy + 1], r.inv[k_dx:k_dx + 1], dm)
+        else:
+            _wgrad_bf16(gw_dn, dm, acts)
+        dy = mm8(dgu8, wq_gu.wT8, r.inv[k_gdy:k_gdy + 1], wq_gu.inv)
+        if ctx.wgrad_fp8:
+            _wgrad_f8(gw_gu, dgu8, ys, r.inv[k_gdy:k_gdy + 1], r.inv[k_gx:k_gx + 1], dgu)
+        else:
+            _wgrad_bf16(gw_gu, dgu, ys)
+        return (dy,) + (None,) * 10
 
 
 class Fp8Linears:
@@ -397,30 +413,27 @@ class Fp8Linears:
 
     def x_target(self, key: str) -> Optional[QuantTarget]:
         """Fused-producer target for the projection ``key``'s input (e4m3)."""
-        if self.wgrad_fp8:  # that path also needs x8^T: keep the separate cast+transpose
-            return None
         return self.recipe.target(self._slots(key)[0], E4M3)
 
     def dy_target(self, key: str) -> Optional[QuantTarget]:
         """Fused-producer target for the gradient of projection ``key``'s output (e5m2)."""
-        if self.wgrad_fp8:
-            return None
         return self.recipe.target(self._slots(key)[1], E5M2)
 
     def rope_ok(self, x: torch.Tensor, w: torch.Tensor, hd: int, rope_cols: int) -> bool:
         """Can the q|k|v projection run as fp8 GEMM + fused RoPE (own kernel)."""
-        return (fp8_fused_epilogues() and not self.wgrad_fp8 and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
+        return (fp8_fused_epilogues() and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
                 and x.shape[1] % 128 == 0 and w.shape[0] % 8 == 0 and hd in (32, 64) and rope_cols % 64 == 0)
 
     def rope(self, key: str, x, w, gw, version: int, x8, cos, sin, T: int, hd: int, rope_cols: int):
         kx, kdy = self._slots(key)
         wq = self.weights[key].get(w, version)
-        return Fp8RopeFn.apply(x, w, gw, wq, self.recipe, kx, kdy, x8, cos, sin, int(T), int(hd), int(rope_cols))
+        return Fp8RopeFn.apply(x, w, gw, wq, self.recipe, kx, kdy, x8, cos, sin, int(T), int(hd), int(rope_cols),
+                               self.wgrad_fp8)
 
     def mlp_ok(self, y: torch.Tensor, w_gu: torch.Tensor, w_dn: torch.Tensor) -> bool:
         """Can the MLP run as fp8 GEMMs with the fused SwiGLU forward / backward epilogues."""
         F = w_gu.shape[0] // 2
-        return (fp8_fused_epilogues() and not self.wgrad_fp8 and y.is_cuda and y.dim() == 2 and y.stride(1) == 1
+        return (fp8_fused_epilogues() and y.is_cuda and y.dim() == 2 and y.stride(1) == 1
                 and y.shape[1] % 128 == 0 and F % 128 == 0 and w_dn.shape[1] == F and w_dn.shape[0] % 128 == 0)
 
     def mlp(self, kgu: str, kdn: str, y, w_gu, w_dn, gw_gu, gw_dn, version: int, y8=None):
@@ -428,7 +441,8 @@ class Fp8Linears:
         k_dx, k_ddy = self._slots(kdn)
         wq_gu = self.weights[kgu].get(w_gu, version)
         wq_dn = self.weights[kdn].get(w_dn, version)
-        return Fp8MLPFn.apply(y, w_gu, w_dn, gw_gu, gw_dn, wq_gu, wq_dn, self.recipe, (k_gx, k_gdy, k_dx, k_ddy), y8)
+        return Fp8MLPFn.apply(y, w_gu, w_dn, gw_gu, gw_dn, wq_gu, wq_dn, self.recipe, (k_gx, k_gdy, k_dx, k_ddy), y8,
+                              self.wgrad_fp8)
 
     def __call__(self, key: str, x: torch.Tensor, w: torch.Tensor, gw: Optional[torch.Tensor], version: int,
                  x8: Optional[torch.Tensor] = None):

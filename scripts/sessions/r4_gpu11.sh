@@ -11,4 +11,6 @@ rc=$?; tail -5 $O/probe.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u -m pytest tests/test_gemm_pp_f8_gpu.py -x -q --timeout 120 --timeout-method thread > $O/test.log 2>&1
 rc=$?; tail -15 $O/test.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u scripts/gemm_pp_f8_bench.py --rounds 5 > $O/bench.log 2>&1
-rc=$?; cat $O/bench.log; exit $rc
+rc=$?; cat $O/bench.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests/test_fp8_gpu.py -x -q --timeout 300 --timeout-method thread > $O/fp8test.log 2>&1
+rc=$?; tail -5 $O/fp8test.log; exit $rc

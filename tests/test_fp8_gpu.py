@@ -101,13 +101,14 @@ def test_fp8_linear_close_to_fp32(wgrad_fp8, fp8_gemm):
     assert torch.isfinite(lin.recipe.scale[:2]).all() and (lin.recipe.scale[:2] > 0).all()
 
 
-def test_fp8_training_tracks_bf16(fp8_gemm):
+@pytest.mark.parametrize("wgrad_fp8", [False, True], ids=["wgrad-bf16", "wgrad-fp8"])
+def test_fp8_training_tracks_bf16(fp8_gemm, wgrad_fp8):
     cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=768, num_attention_heads=4,
                                      num_key_value_heads=4, num_hidden_layers=2, vocab_size=512))
     ids = torch.randint(0, 512, (8, 256), device="cuda")
     losses = {}
     for use_fp8 in (False, True):
-        m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16, fp8=use_fp8).init_weights(5)
+        m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16, fp8=use_fp8, fp8_wgrad=wgrad_fp8).init_weights(5)
         opt = FlatAdamW(m.store, lr=3e-3)
         ls = []
         for _ in range(30):
