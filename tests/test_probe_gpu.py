@@ -28,7 +28,7 @@ def _src_index(addr: torch.Tensor) -> torch.Tensor:
 def test_tr8_block_transpose(hip_lib):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    ld = 256  # LDS row pitch (bytes) of a [rows][256 B] image
+    ld = 128  # LDS row pitch (bytes) of a [32 rows][128 B] image (the probe holds 4 KiB)
     lane = torch.arange(64)
     g, j = lane // 16, lane % 16
     q, p = j // 2, j % 2
