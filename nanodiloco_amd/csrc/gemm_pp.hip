@@ -80,6 +80,11 @@ struct PPEpi {
   int64_t ld_gu;
   const float* sa;    // fp8 operands (F8 != 0): per-tensor dequantisation scales, acc *= sa[0] * sb[0]
   const float* sb;
+  uint8_t* q8;          // Q: fp8 output INSTEAD of the bf16 act (PP_SWIGLU, e4m3) / d(gate|up) (PP_DSWIGLU, e5m2)
+  int64_t ld_q8;
+  const float* qscale;  // delayed-scaling scale of that output (device scalar)
+  float* qamax;         // amax partial slots (float bits as ordered ints)
+  int qparts;
 };
 
 // stores per wave per tile epilogue (counted by the vmcnt waits that follow it)
@@ -127,6 +132,7 @@ __device__ __forceinline__ void mma0(const bf16x8& a, const bf16x8& b, f32x4& c)
 // each fragment (the lane's 32 K bytes), unit E8M0 block scales (`one` = 0x7F7F7F7F).  The MFMA's first
 // source is B (cbsz = B's format), its second A (blgp = A's format).
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ i32x8 cat16(const bf16x8& x, const bf16x8& y) {
   const i32x4 a = __builtin_bit_cast(i32x4, x), b = __builtin_bit_cast(i32x4, y);
@@ -180,10 +186,10 @@ __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); 
 // of the tile at (m0, n0) -> the fused output(s).  Exactly NStores<EPI> 16-B buffer stores per wave
 // (the callers' counted waits rely on it); out-of-range lanes drop through the descriptor's record
 // count or an offset sentinel.  `smem` + 2 BUF_B + 4 KiB w: the wave's private C staging region.
-template <int EPI, int HD, int ABL, int F8 = 0>
+template <int EPI, int HD, int ABL, int F8 = 0, int Q = 0>
 __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __restrict__ C, int M, int N,
                                             int64_t ldc, const PPEpi& ep, int m0, int n0, int g, int wn, int w,
-                                            int lane, char* smem, float sc) {
+                                            int lane, char* smem, float sc, float qs, float& qmax) {
   constexpr int STP = (ABL & 32) ? 0 : 2;
 
     // per-lane row offsets derive from an opaque zero: otherwise LICM hoists every row's store
@@ -296,10 +302,30 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
           }
         const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
         const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
-        const uint32_t oy = ok ? (uint32_t)(((int64_t)mr * ep.ld_act + f) * 2) : 0x80000000u;
         __builtin_amdgcn_raw_buffer_store_b128(pair16(g2[0], g2[1]), cr, og, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(pair16(u2[0], u2[1]), cr, ou, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(pair16(y2[0], y2[1]), ar, oy, 0, 0);
+        if constexpr (Q != 0) {
+          // e4m3 act (bitwise a separate cast of the bf16 act, which is not written): the lane's 8 units in
+          // column order (pair16's permutation on the fp32 values), bf16-rounded, scaled, one 8-B store
+          const auto qr = rsrc(ep.q8 + (int64_t)m0 * ep.ld_q8, (uint32_t)((int64_t)rows * ep.ld_q8));
+          float e[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(y2[0][r]), __float_as_uint(y2[1][r]),
+                                                              false, false);
+            e[r] = rbf(__uint_as_float(sw[0]));
+            e[4 + r] = rbf(__uint_as_float(sw[1]));
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) qmax = fmaxf(qmax, fabsf(e[j]));
+          const uint2 o = uint2{cvt4<0>(e[0] * qs, e[1] * qs, e[2] * qs, e[3] * qs),
+                                cvt4<0>(e[4] * qs, e[5] * qs, e[6] * qs, e[7] * qs)};
+          const uint32_t oq = ok ? (uint32_t)((int64_t)mr * ep.ld_q8 + f) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, o), qr, oq, 0, 0);
+        } else {
+          const uint32_t oy = ok ? (uint32_t)(((int64_t)mr * ep.ld_act + f) * 2) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b128(pair16(y2[0], y2[1]), ar, oy, 0, 0);
+        }
       }
     } else {  // PP_DSWIGLU: acc = d(act)[m][f]; C = d(gate | up) [M, 2N]
       const auto cr = rsrc(C + (int64_t)m0 * ldc, (uint32_t)((int64_t)rows * ldc * 2));
@@ -307,7 +333,7 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
       // the 16 (row block, column pair) steps read gate / up from HBM: their loads run PF steps ahead
       // (2 x PF x 4 VGPRs, taken from the next K-tile's fragment registers, free here) instead of one
       // -- one exposed HBM round trip per tile instead of per step
-      constexpr int PF = DSW_PF;
+      constexpr int PF = Q != 0 ? 4 : DSW_PF;  // the fp8-output form needs the registers
       u32x4 gq[PF], uq[PF];
       auto gu_off = [&](int st, int half) -> uint32_t {
         const int a = st >> 1, bp = st & 1;
@@ -364,35 +390,55 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
             du[e] = d * gg * sg;
             dg[e] = d * uu * sg * (1.f + gg * (1.f - sg));
           }
-          const u32x4 og4 = u32x4{pack2(dg[0], dg[1]), pack2(dg[2], dg[3]), pack2(dg[4], dg[5]), pack2(dg[6], dg[7])};
-          const u32x4 ou4 = u32x4{pack2(du[0], du[1]), pack2(du[2], du[3]), pack2(du[4], du[5]), pack2(du[6], du[7])};
-          if constexpr ((ABL & 256) == 0) {
-            // full-line stores as in the plain epilogue: d(gate) rows 0-15 and d(up) rows 16-31 of the
-            // wave's 4-KiB LDS staging region; after both column halves, 16 rows x 128 B per output
-            char* stg = smem + 2 * BUF_B + w * 4096;
-            const int ch = (2 * bp + (q & 1)) * 2 + (q >> 1);
-            *reinterpret_cast<u32x4*>(stg + r16 * 128 + ((ch ^ (r16 & 7)) << 4)) = og4;
-            *reinterpret_cast<u32x4*>(stg + (16 + r16) * 128 + ((ch ^ (r16 & 7)) << 4)) = ou4;
-            if (bp == 1) {
-              asm volatile("" ::: "memory");
-              const int lc = (lane + z) & 7;
-              const int col = n0 + wn * 64 + lc * 8;
+          if constexpr (Q != 0) {
+            // e5m2 d(gate | up) instead of the bf16 one: bf16-rounded, scaled, two 8-B stores
+            const auto qr = rsrc(ep.q8 + (int64_t)m0 * ep.ld_q8, (uint32_t)((int64_t)rows * ep.ld_q8));
 #pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const int rr = i * 8 + ((lane + z) >> 3);  // staging row: i < 2 gate, else up
-                const u32x4 d = *reinterpret_cast<const u32x4*>(stg + rr * 128 + ((lc ^ (rr & 7)) << 4));
-                const int grow = g * 128 + a * 16 + (rr & 15);
-                const uint32_t off =
-                    col < N ? (uint32_t)(((int64_t)grow * ldc + (i >= 2 ? N : 0) + col) * 2) : 0x80000000u;
-                __builtin_amdgcn_raw_buffer_store_b128(d, cr, off, 0, STP);
-              }
-              asm volatile("" ::: "memory");
+            for (int e = 0; e < 8; ++e) {
+              dg[e] = rbf(dg[e]);
+              du[e] = rbf(du[e]);
+              qmax = fmaxf(qmax, fmaxf(fabsf(dg[e]), fabsf(du[e])));
             }
+            const uint2 og8 = uint2{cvt4<1>(dg[0] * qs, dg[1] * qs, dg[2] * qs, dg[3] * qs),
+                                    cvt4<1>(dg[4] * qs, dg[5] * qs, dg[6] * qs, dg[7] * qs)};
+            const uint2 ou8 = uint2{cvt4<1>(du[0] * qs, du[1] * qs, du[2] * qs, du[3] * qs),
+                                    cvt4<1>(du[4] * qs, du[5] * qs, du[6] * qs, du[7] * qs)};
+            const uint32_t cg = ok ? (uint32_t)((int64_t)mr * ep.ld_q8 + f) : 0x80000000u;
+            const uint32_t cu = ok ? (uint32_t)((int64_t)mr * ep.ld_q8 + N + f) : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, og8), qr, cg, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, ou8), qr, cu, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);  // one step at a time: bounded epilogue registers
           } else {
-            const uint32_t cg = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
-            const uint32_t cu = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
-            __builtin_amdgcn_raw_buffer_store_b128(og4, cr, cg, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(ou4, cr, cu, 0, 0);
+            const u32x4 og4 = u32x4{pack2(dg[0], dg[1]), pack2(dg[2], dg[3]), pack2(dg[4], dg[5]), pack2(dg[6], dg[7])};
+            const u32x4 ou4 = u32x4{pack2(du[0], du[1]), pack2(du[2], du[3]), pack2(du[4], du[5]), pack2(du[6], du[7])};
+            if constexpr ((ABL & 256) == 0) {
+              // full-line stores as in the plain epilogue: d(gate) rows 0-15 and d(up) rows 16-31 of the
+              // wave's 4-KiB LDS staging region; after both column halves, 16 rows x 128 B per output
+              char* stg = smem + 2 * BUF_B + w * 4096;
+              const int ch = (2 * bp + (q & 1)) * 2 + (q >> 1);
+              *reinterpret_cast<u32x4*>(stg + r16 * 128 + ((ch ^ (r16 & 7)) << 4)) = og4;
+              *reinterpret_cast<u32x4*>(stg + (16 + r16) * 128 + ((ch ^ (r16 & 7)) << 4)) = ou4;
+              if (bp == 1) {
+                asm volatile("" ::: "memory");
+                const int lc = (lane + z) & 7;
+                const int col = n0 + wn * 64 + lc * 8;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  const int rr = i * 8 + ((lane + z) >> 3);  // staging row: i < 2 gate, else up
+                  const u32x4 d = *reinterpret_cast<const u32x4*>(stg + rr * 128 + ((lc ^ (rr & 7)) << 4));
+                  const int grow = g * 128 + a * 16 + (rr & 15);
+                  const uint32_t off =
+                      col < N ? (uint32_t)(((int64_t)grow * ldc + (i >= 2 ? N : 0) + col) * 2) : 0x80000000u;
+                  __builtin_amdgcn_raw_buffer_store_b128(d, cr, off, 0, STP);
+                }
+                asm volatile("" ::: "memory");
+              }
+            } else {
+              const uint32_t cg = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
+              const uint32_t cu = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
+              __builtin_amdgcn_raw_buffer_store_b128(og4, cr, cg, 0, 0);
+              __builtin_amdgcn_raw_buffer_store_b128(ou4, cr, cu, 0, 0);
+            }
           }
         }
       }
@@ -405,7 +451,7 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
 // LDS loads: bitwise the same, 1.004-1.011x on the fused kernels, profiles/r4_gdma_ab.md)
 // F8 (fp8 operands, one 16x16x128 MFMA per 128-deep K-tile of the same 128-B LDS rows): 0 bf16; 1 A e4m3,
 // B e4m3 (forward); 2 A e5m2, B e4m3 (input gradient).  A / B are then byte arrays, lda / ldb in bytes.
-template <int EPI, int HD, int ABL = 0, int F8 = 0>
+template <int EPI, int HD, int ABL = 0, int F8 = 0, int Q = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restrict__ A_, const bf16_t* __restrict__ B_,
                                                          bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
                                                          int64_t ldb, int64_t ldc, PPEpi ep, int GM) {
@@ -431,6 +477,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
   const int g = w >> 2, wn = w & 3;
   const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
   const float sc = F8 != 0 ? ep.sa[0] * ep.sb[0] : 1.f;  // fp8 dequantisation of the accumulator
+  const float qs = Q != 0 ? ep.qscale[0] : 1.f;           // Q: the fp8 output's scale
+  float qmax = 0.f;                                        // Q: running amax of the fp8 output
   int one = 0;  // unit E8M0 block scales of the fp8 MFMA
   if constexpr (F8 != 0) asm volatile("v_mov_b32 %0, 0x7f7f7f7f" : "=v"(one));
 
@@ -615,7 +663,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
       } else {
         int m0, n0;
         coords(first + (lt - 1) * G, m0, n0);
-        pp_epilogue<EPI, HD, ABL, F8>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc);
+        pp_epilogue<EPI, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
       }
       // the accumulators are free only after the epilogue has read them: keep the fragment reads
       // (96 VGPRs) from being hoisted into it
@@ -667,9 +715,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
   if constexpr ((ABL & 8) == 0) {
     int m0, n0;
     coords(first + (my_tiles - 1) * G, m0, n0);
-    pp_epilogue<EPI, HD, ABL, F8>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc);
+    pp_epilogue<EPI, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
   }
   if (g == 0 && !(ABL & 4)) bar();  // group 1 ran one barrier more
+  if constexpr (Q != 0) {  // one amax partial per wave (vector atomic on an ordered-int view)
+    qmax = wave_max(qmax);
+    if (lane == 0) atomicMax(reinterpret_cast<int*>(ep.qamax + (blockIdx.x * 8 + w) % ep.qparts), __float_as_int(qmax));
+  }
 }
 
 
@@ -695,17 +747,17 @@ int g_pp_variant = [] {
 }();
 
 
-template <int EPI, int HD, int ABL, int F8 = 0>
+template <int EPI, int HD, int ABL, int F8 = 0, int Q = 0>
 int launch_pp_v(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
                 const PPEpi& ep, hipStream_t s) {
   const size_t lds = 2 * (size_t)BUF_B + ((ABL & 256) ? 0 : 8 * 4096);  // 128 KiB + 32 KiB C staging
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<EPI, HD, ABL, F8>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<EPI, HD, ABL, F8, Q>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return (int)attr;
   const int tcols = EPI == PP_SWIGLU ? 128 : TN;
   const int tiles = ((M + TM - 1) / TM) * ((N + tcols - 1) / tcols);
   const int grid = tiles < num_cus_pp() ? tiles : num_cus_pp();
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, HD, ABL, F8>), dim3(grid), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, HD, ABL, F8, Q>), dim3(grid), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
                      (bf16_t*)C, M, N, K, lda, ldb, ldc, ep, g_pp_group_m);
   ND_LAUNCH_CHECK();
 }
@@ -844,6 +896,37 @@ ND_API int nd_gemm_pp_dswiglu_f8(const void* A, const void* B, const void* gu, v
   PPEpi ep{};
   ep.gu = (const bf16_t*)gu; ep.ld_gu = ld_gu; ep.sa = sa; ep.sb = sb;
   return launch_pp8<PP_DSWIGLU>(fa, A, B, dgu, M, F, K, lda, ldb, ld_dgu, ep, s);
+}
+
+// Q forms: the SwiGLU output as e4m3 act8 [M, F] (ld_q8) INSTEAD of the bf16 act / the d(gate|up) as e5m2
+// dgu8 [M, 2F] INSTEAD of the bf16 dgu, with the delayed-scaling scale `qscale` and amax into `qparts`
+// partial slots -- bitwise a separate nd_fp8_cast of the bf16 tensor the plain form writes.
+ND_API int nd_gemm_pp_swiglu_f8q(const void* A, const void* B, void* gu, void* act8, int M, int F, int K, int64_t lda,
+                                 int64_t ldb, int64_t ldc, int64_t ld_q8, const float* sa, const float* sb,
+                                 const float* qscale, float* qamax, int qparts, hipStream_t s) {
+  if (!pp_f8_ok(M, F, K, lda, ldb, ldc, 0, sa, sb) || ldc < 2 * (int64_t)F || ld_q8 % 8 || ld_q8 < F || !qscale ||
+      !qamax || qparts < 1 || (int64_t)2 * F * ldb >= (1ll << 31) || (int64_t)TM * ld_q8 >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  PPEpi ep{};
+  ep.sa = sa; ep.sb = sb; ep.q8 = (uint8_t*)act8; ep.ld_q8 = ld_q8; ep.qscale = qscale; ep.qamax = qamax;
+  ep.qparts = qparts;
+  return launch_pp_v<PP_SWIGLU, 64, 0, 1, 1>(A, B, gu, M, F, K, lda, ldb, ldc, ep, s);
+}
+
+ND_API int nd_gemm_pp_dswiglu_f8q(const void* A, const void* B, const void* gu, void* dgu8, int M, int F, int K,
+                                  int64_t lda, int64_t ldb, int64_t ld_gu, int64_t ld_q8, const float* sa,
+                                  const float* sb, int fa, const float* qscale, float* qamax, int qparts,
+                                  hipStream_t s) {
+  if (!pp_f8_ok(M, F, K, lda, ldb, 2 * (int64_t)F, fa, sa, sb) || ld_gu % 8 || ld_gu < 2 * (int64_t)F ||
+      ld_q8 % 8 || ld_q8 < 2 * (int64_t)F || !qscale || !qamax || qparts < 1 || (int64_t)TM * ld_gu * 2 >= (1ll << 31) ||
+      (int64_t)TM * ld_q8 >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  PPEpi ep{};
+  ep.gu = (const bf16_t*)gu; ep.ld_gu = ld_gu; ep.sa = sa; ep.sb = sb; ep.q8 = (uint8_t*)dgu8; ep.ld_q8 = ld_q8;
+  ep.qscale = qscale; ep.qamax = qamax; ep.qparts = qparts;
+  // C (the bf16 dgu) is not written: the Q epilogue stores through ep.q8 only
+  return fa == 0 ? launch_pp_v<PP_DSWIGLU, 64, 0, 1, 1>(A, B, dgu8, M, F, K, lda, ldb, 2 * (int64_t)F, ep, s)
+                 : launch_pp_v<PP_DSWIGLU, 64, 0, 2, 1>(A, B, dgu8, M, F, K, lda, ldb, 2 * (int64_t)F, ep, s);
 }
 
 ND_API int nd_gemm_pp_set_variant(int v) {

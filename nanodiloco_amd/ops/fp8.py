@@ -33,8 +33,9 @@ from typing import Dict, Optional
 import torch
 
 from . import _ext
-from .gemm import (f8_nt_supported, gemm_nt_f8, gemm_pp_dswiglu_f8, gemm_pp_f8, gemm_pp_rope_f8, gemm_pp_swiglu_f8,
-                   pp_f8_supported, wgrad, wgrad_f8, wgrad_f8_supported, wgrad_supported)
+from .gemm import (f8_nt_supported, gemm_nt_f8, gemm_pp_dswiglu_f8, gemm_pp_dswiglu_f8q, gemm_pp_f8, gemm_pp_rope_f8,
+                   gemm_pp_swiglu_f8, gemm_pp_swiglu_f8q, pp_f8_supported, wgrad, wgrad_f8, wgrad_f8_supported,
+                   wgrad_supported)
 
 E4M3, E5M2 = 0, 1
 FMAX = {E4M3: 448.0, E5M2: 57344.0}
@@ -304,14 +305,16 @@ def _wgrad_bf16(gw, dy, x):
         gw.add_(torch.mm(dy.t(), x).float())
 
 
-def _wgrad_f8(gw, dy8, x8, inv_dy, inv_x, dy):
+def _wgrad_f8(gw, dy8, x8, inv_dy, inv_x, dy=None):
     """gw += dy^T x from the fp8 operands (own kernel, csrc/gemm_wgrad.hip wgrad8_pp_kernel); shapes it does
-    not take fall back to the bf16 kernel on the dequantised input."""
+    not take fall back to the bf16 kernel on the dequantised operands (``dy``: the bf16 gradient if kept)."""
     if gw is None:
         return
     if wgrad_f8_supported(gw, dy8, x8):
         wgrad_f8(gw, dy8, x8, inv_dy, inv_x)
     else:
+        if dy is None:
+            dy = (dy8.float() * inv_dy).to(torch.bfloat16)
         _wgrad_bf16(gw, dy, (x8.float() * inv_x).to(dy.dtype))
 
 
@@ -365,8 +368,16 @@ class Fp8MLPFn(torch.autograd.Function):
         k_gx, k_gdy, k_dx, k_ddy = ks
         if y8 is None or y8.shape != y.shape:
             y8 = recipe.quantize(y, k_gx, E4M3)
-        gu, act = gemm_pp_swiglu_f8(y8, wq_gu.w8, recipe.inv[k_gx:k_gx + 1], wq_gu.inv)
-        act8 = recipe.quantize(act, k_dx, E4M3)
+        # with fp8 weight gradients nothing needs the bf16 act: once the slot has a scale, the epilogue writes
+        # act8 directly (bitwise the cast of the bf16 act) and no bf16 act exists
+        q = wgrad_fp8 and recipe.ready[k_dx] and _FUSED["enabled"] and y.shape[0] % 128 == 0
+        if q:
+            gu, act8 = gemm_pp_swiglu_f8q(y8, wq_gu.w8, recipe.inv[k_gx:k_gx + 1], wq_gu.inv,
+                                          recipe.scale[k_dx:k_dx + 1], recipe.amax[k_dx])
+            act = None
+        else:
+            gu, act = gemm_pp_swiglu_f8(y8, wq_gu.w8, recipe.inv[k_gx:k_gx + 1], wq_gu.inv)
+            act8 = recipe.quantize(act, k_dx, E4M3)
         m = mm8(act8, wq_dn.w8, recipe.inv[k_dx:k_dx + 1], wq_dn.inv)
         # fp8 weight gradients keep the fp8 operands (y8, act8) instead of the bf16 ones
         ctx.save_for_backward(y8 if wgrad_fp8 else y, gu, act8 if wgrad_fp8 else act)
@@ -382,8 +393,14 @@ class Fp8MLPFn(torch.autograd.Function):
         k_gx, k_gdy, k_dx, k_ddy = ctx.ks
         dm = dm.contiguous()
         dm8 = _dy8(r, k_ddy, dm)
-        dgu = gemm_pp_dswiglu_f8(dm8, wq_dn.wT8, r.inv[k_ddy:k_ddy + 1], wq_dn.inv, gu)
-        dgu8 = r.quantize(dgu, k_gdy, E5M2)
+        if ctx.wgrad_fp8 and r.ready[k_gdy] and _FUSED["enabled"] and dm.shape[0] % 128 == 0:
+            # only the e5m2 d(gate|up) is consumed (dgrad and fp8 wgrad): the epilogue writes it directly
+            dgu8 = gemm_pp_dswiglu_f8q(dm8, wq_dn.wT8, r.inv[k_ddy:k_ddy + 1], wq_dn.inv, gu,
+                                       r.scale[k_gdy:k_gdy + 1], r.amax[k_gdy])
+            dgu = None
+        else:
+            dgu = gemm_pp_dswiglu_f8(dm8, wq_dn.wT8, r.inv[k_ddy:k_ddy + 1], wq_dn.inv, gu)
+            dgu8 = r.quantize(dgu, k_gdy, E5M2)
         if ctx.wgrad_fp8:
             _wgrad_f8(gw_dn, dm8, acts, r.inv[k_ddy:k_ddy + 1], r.inv[k_dx:k_dx + 1], dm)
         else:

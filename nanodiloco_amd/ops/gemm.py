@@ -191,6 +191,33 @@ def gemm_pp_dswiglu_f8(dy, w_down_t, sa, sb, gu, dgu_out=None):
     return dgu
 
 
+def gemm_pp_swiglu_f8q(a, w_gu, sa, sb, qscale, qamax, gu_out=None, act8_out=None):
+    """As ``gemm_pp_swiglu_f8`` but the SwiGLU output is written ONLY as e4m3 act8 = fp8(bf16(act) * qscale)
+    (bitwise a separate cast of the bf16 act), amax folded into the ``qamax`` partial slots."""
+    M, K = a.shape
+    F = w_gu.shape[0] // 2
+    gu = gu_out if gu_out is not None else torch.empty(M, 2 * F, dtype=torch.bfloat16, device=a.device)
+    act8 = act8_out if act8_out is not None else torch.empty(M, F, dtype=torch.float8_e4m3fn, device=a.device)
+    _ext.check(_ext.lib().nd_gemm_pp_swiglu_f8q(_ext.ptr(a), _ext.ptr(w_gu), _ext.ptr(gu), _ext.ptr(act8), M, F, K,
+                                                a.stride(0), w_gu.stride(0), gu.stride(0), act8.stride(0),
+                                                _ext.ptr(sa), _ext.ptr(sb), _ext.ptr(qscale), _ext.ptr(qamax),
+                                                qamax.numel(), _ext.stream_ptr(a.device)), "nd_gemm_pp_swiglu_f8q")
+    return gu, act8
+
+
+def gemm_pp_dswiglu_f8q(dy, w_down_t, sa, sb, gu, qscale, qamax, dgu8_out=None):
+    """As ``gemm_pp_dswiglu_f8`` but d(gate|up) is written ONLY as e5m2 dgu8 = fp8(bf16(dgu) * qscale)."""
+    M, K = dy.shape
+    F = w_down_t.shape[0]
+    dgu8 = dgu8_out if dgu8_out is not None else torch.empty(M, 2 * F, dtype=torch.float8_e5m2, device=dy.device)
+    _ext.check(_ext.lib().nd_gemm_pp_dswiglu_f8q(_ext.ptr(dy), _ext.ptr(w_down_t), _ext.ptr(gu), _ext.ptr(dgu8), M, F,
+                                                 K, dy.stride(0), w_down_t.stride(0), gu.stride(0), dgu8.stride(0),
+                                                 _ext.ptr(sa), _ext.ptr(sb), _F8_FMT[dy.dtype], _ext.ptr(qscale),
+                                                 _ext.ptr(qamax), qamax.numel(), _ext.stream_ptr(dy.device)),
+               "nd_gemm_pp_dswiglu_f8q")
+    return dgu8
+
+
 def gemm_w128(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     """out[M, N] = a[M, K] . b[N, K]^T on the one-wave-per-SIMD kernel (csrc/gemm_w128.hip: 4 waves,
     128 x 128 outputs per wave, one continuous MFMA stream per K-tile -- the hipBLASLt K-loop shape)."""

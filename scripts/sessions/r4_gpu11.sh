@@ -13,4 +13,13 @@ rc=$?; tail -15 $O/test.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u scripts/gemm_pp_f8_bench.py --rounds 5 > $O/bench.log 2>&1
 rc=$?; cat $O/bench.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u -m pytest tests/test_fp8_gpu.py -x -q --timeout 300 --timeout-method thread > $O/fp8test.log 2>&1
-rc=$?; tail -5 $O/fp8test.log; exit $rc
+rc=$?; tail -5 $O/fp8test.log; [ $rc -eq 0 ] || exit $rc
+v() { grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' $1 | tr '\n' ' '; }
+for r in 1 2; do
+  timeout -k 10 300 python bench.py --steps 6 --warmup 2 > $O/bf16_$r.log 2>&1 || { tail -3 $O/bf16_$r.log; exit 1; }
+  echo "bf16 r=$r $(v $O/bf16_$r.log)"
+  timeout -k 10 300 python bench.py --steps 6 --warmup 2 --fp8 > $O/f8_$r.log 2>&1 || { tail -3 $O/f8_$r.log; exit 1; }
+  echo "fp8 (wgrad bf16) r=$r $(v $O/f8_$r.log)"
+  timeout -k 10 300 python bench.py --steps 6 --warmup 2 --fp8 --fp8-wgrad > $O/f8w_$r.log 2>&1 || { tail -3 $O/f8w_$r.log; exit 1; }
+  echo "fp8 + fp8 wgrad r=$r $(v $O/f8w_$r.log)"
+done

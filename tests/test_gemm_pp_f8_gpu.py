@@ -166,3 +166,38 @@ def test_wgrad_f8_strided_and_deterministic():
     ref = (dy8.float().t() @ x8.float()) * (sdy * sx)
     assert rel(out[0], ref) < 2e-3
     assert torch.equal(out[0], out[1])
+
+
+# ---------------------------------------------------------------- fp8 side outputs of the SwiGLU epilogues
+def _cast(x, scale, dt):
+    from nanodiloco_amd.ops import fp8
+    return fp8.cast(x, scale, 0 if dt == E4 else 1)
+
+
+@pytest.mark.parametrize("M,F", [(1024, 768), (1000, 640)])
+def test_gemm_pp_swiglu_f8q_bitwise(M, F):
+    """act8 from the epilogue == a separate cast of the plain form's bf16 act (bytes and amax)."""
+    K = 1024
+    x8, sa = q8(torch.randn(M, K, device=DEV), E4)
+    w8, sb = q8(torch.randn(2 * F, K, device=DEV) * 0.05, E4)
+    gu, act = G.gemm_pp_swiglu_f8(x8, w8, sa, sb)
+    qs = torch.tensor([37.0], device=DEV)
+    amax = torch.zeros(64, device=DEV)
+    gu2, act8 = G.gemm_pp_swiglu_f8q(x8, w8, sa, sb, qs, amax)
+    assert torch.equal(gu, gu2)
+    assert torch.equal(act8.view(torch.uint8), _cast(act, qs, E4).view(torch.uint8))
+    assert amax.max().item() == act.float().abs().max().item()
+
+
+@pytest.mark.parametrize("ddt", [E5, E4], ids=["e5m2", "e4m3"])
+def test_gemm_pp_dswiglu_f8q_bitwise(ddt):
+    M, F, K = 1000, 640, 1024
+    gu = torch.randn(M, 2 * F, device=DEV).bfloat16()
+    dy8, sa = q8(torch.randn(M, K, device=DEV), ddt)
+    wdt8, sb = q8(torch.randn(F, K, device=DEV) * 0.05, E4)
+    dgu = G.gemm_pp_dswiglu_f8(dy8, wdt8, sa, sb, gu)
+    qs = torch.tensor([900.0], device=DEV)
+    amax = torch.zeros(64, device=DEV)
+    dgu8 = G.gemm_pp_dswiglu_f8q(dy8, wdt8, sa, sb, gu, qs, amax)
+    assert torch.equal(dgu8.view(torch.uint8), _cast(dgu, qs, E5).view(torch.uint8))
+    assert amax.max().item() == dgu.float().abs().max().item()
