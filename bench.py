@@ -81,10 +81,13 @@ def parse():
     ap.add_argument("--fused-mlp", type=int, default=1, choices=[0, 1],
                     help="SwiGLU in the gate|up GEMM epilogue and its backward in the down dgrad epilogue")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
-    ap.add_argument("--fp8-wgrad", action="store_true", help="with --fp8: weight-gradient GEMM in fp8 too")
-    ap.add_argument("--fp8-gemm", default="pp", choices=["pp", "hip", "hipblaslt"],
-                    help="with --fp8: forward / input-gradient fp8 GEMMs on the own ping-pong fp8 kernel (pp, "
-                         "default), the round-2 fp8 kernel (hip) or hipBLASLt")
+    ap.add_argument("--fp8-wgrad", type=int, default=1, choices=[0, 1],
+                    help="with --fp8: weight-gradient GEMMs in fp8 too (own kernel on the token-major fp8 "
+                         "operands; default on)")
+    ap.add_argument("--fp8-gemm", default="auto", choices=["auto", "pp", "hip", "hipblaslt"],
+                    help="with --fp8: forward / input-gradient fp8 GEMMs: auto (default: own fp8 ping-pong kernel "
+                         "with the fused epilogues, hipBLASLt for the long-K N<=1024 plain products), pp (own "
+                         "kernel for all), hip (round-2 fp8 kernel) or hipblaslt")
     ap.add_argument("--fp8-fused-epi", type=int, default=1, choices=[0, 1],
                     help="with --fp8 and --fp8-gemm pp: RoPE / SwiGLU fused into the fp8 GEMM epilogues")
     ap.add_argument("--fp8-keep-fused", default="none", choices=["none", "rope", "mlp", "both"],
@@ -119,7 +122,7 @@ def main():
         warmup_steps=100, total_steps=H * max(1, -(-10_000 // H)), inner_steps=H, lr=4e-4, outer_lr=0.7,
         llama_config_file=a.model, data="synthetic", ops=a.ops, backend=a.backend, inner_dp=a.inner_dp,
         comm_dtype=a.comm_dtype, bucket_mb=a.bucket_mb, overlap_outer=a.overlap_outer, fp8=a.fp8,
-        fp8_wgrad=a.fp8_wgrad, fp8_keep_fused=a.fp8_keep_fused, tuned_gemm=not a.no_tuned_gemm and not a.tuned_gemm_file,
+        fp8_wgrad=bool(a.fp8_wgrad), fp8_keep_fused=a.fp8_keep_fused, tuned_gemm=not a.no_tuned_gemm and not a.tuned_gemm_file,
         hip_graph="on" if a.hip_graph else "off", wgrad_overlap=bool(a.wgrad_overlap), log_every=0, wandb="off",
         phase_timing=False, force_collectives=a.backend != "auto" and world == 1)
     tr = Trainer(targs)

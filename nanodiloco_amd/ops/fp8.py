@@ -48,15 +48,17 @@ _FUSED = {"enabled": True}
 # also carries the fused RoPE / SwiGLU epilogues; "hip": the round-2 one-wave-per-SIMD fp8 kernel
 # (csrc/gemm_f8.hip); "hipblaslt": torch._scaled_mm.  Shapes the own kernels do not take fall back to
 # torch._scaled_mm.
-_GEMM = {"backend": "pp"}
+_GEMM = {"backend": "auto"}
 # fp8 projections with their fused epilogues on the own fp8 GEMM: q|k|v + RoPE, gate|up + SwiGLU and the
 # down input gradient + SwiGLU backward (backend "pp" only)
 _EPI = {"enabled": True}
 
 
 def set_fp8_gemm(backend: str) -> None:
-    """fp8 forward / input-gradient GEMMs: "pp" (default), "hip" or "hipblaslt"."""
-    if backend not in ("pp", "hip", "hipblaslt"):
+    """fp8 forward / input-gradient GEMMs: "auto" (default: the own fp8 kernel for the fused-epilogue
+    products and every plain product it matches, hipBLASLt for the long-K N <= 1024 plain products),
+    "pp" (the own kernel for everything), "hip" or "hipblaslt"."""
+    if backend not in ("auto", "pp", "hip", "hipblaslt"):
         raise ValueError(backend)
     _GEMM["backend"] = backend
 
@@ -67,7 +69,13 @@ def set_fp8_fused_epilogues(enabled: bool) -> None:
 
 
 def fp8_fused_epilogues() -> bool:
-    return _EPI["enabled"] and _GEMM["backend"] == "pp"
+    return _EPI["enabled"] and _GEMM["backend"] in ("auto", "pp")
+
+
+def _own_plain(a8: torch.Tensor, b8: torch.Tensor) -> bool:
+    """"auto": plain products the own fp8 kernel runs at >= 0.95x hipBLASLt (profiles/r4_fp8_pp.md: K = 1024
+    0.95-1.07x; N = 1024 with K = 2688-5376 0.80-0.82x, where hipBLASLt's stream-K kernels win)."""
+    return not (b8.shape[0] <= 1024 and a8.shape[1] > 1024)
 
 
 def fp8_gemm_backend() -> str:
@@ -76,7 +84,8 @@ def fp8_gemm_backend() -> str:
 
 def mm8(a8: torch.Tensor, b8: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) -> torch.Tensor:
     """bf16 sa * sb * a8 . b8^T (a8 [M, K], b8 [N, K] fp8)."""
-    if _GEMM["backend"] == "pp" and pp_f8_supported(a8, b8):
+    be = _GEMM["backend"]
+    if (be == "pp" or (be == "auto" and _own_plain(a8, b8))) and pp_f8_supported(a8, b8):
         return gemm_pp_f8(a8, b8, sa, sb)
     if _GEMM["backend"] == "hip" and f8_nt_supported(a8, b8):
         return gemm_nt_f8(a8, b8, sa, sb)

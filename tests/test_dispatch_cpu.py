@@ -10,9 +10,11 @@ from nanodiloco_amd.ops import gemm as G
 
 def test_fp8_gemm_backend_switch():
     old = fp8.fp8_gemm_backend()
-    assert old == "pp"  # the own fp8 ping-pong kernel with fused epilogues (profiles/r4_fp8_pp.md)
+    assert old == "auto"  # own fp8 ping-pong kernel + fused epilogues, hipBLASLt for long-K narrow plain products
     assert fp8.fp8_fused_epilogues()
     try:
+        fp8.set_fp8_gemm("pp")
+        assert fp8.fp8_fused_epilogues()
         fp8.set_fp8_gemm("hip")
         assert fp8.fp8_gemm_backend() == "hip"
         assert not fp8.fp8_fused_epilogues()  # the fused fp8 epilogues live in the pp kernel only
@@ -93,3 +95,11 @@ def test_proj_gemm_modes():
             L.set_proj_gemm("cublas")
     finally:
         L.set_proj_gemm("blas")
+
+
+def test_fp8_auto_dispatch_rule():
+    a = torch.zeros(4096, 1024, dtype=torch.float8_e4m3fn)
+    assert fp8._own_plain(a, torch.zeros(1024, 1024, dtype=torch.float8_e4m3fn))  # K = 1024: own kernel
+    assert fp8._own_plain(a, torch.zeros(2688, 1024, dtype=torch.float8_e4m3fn))
+    long_k = torch.zeros(4096, 5376, dtype=torch.float8_e5m2)
+    assert not fp8._own_plain(long_k, torch.zeros(1024, 5376, dtype=torch.float8_e4m3fn))  # hipBLASLt

@@ -68,7 +68,7 @@ def test_fp8_weight_current_scaling(shape):
     assert wq.get(w, version=0) is wq and wq.version == 0
 
 
-@pytest.fixture(params=["pp", "hipblaslt", "hip"])
+@pytest.fixture(params=["auto", "pp", "hipblaslt", "hip"])
 def fp8_gemm(request):
     """The fp8 GEMM backends: the own ping-pong kernel (default; with the fused RoPE / SwiGLU epilogues
     in the model), hipBLASLt, and the round-2 own kernel (csrc/gemm_f8.hip)."""
