@@ -18,5 +18,9 @@ for r in 1 2; do
   timeout -k 10 300 python bench.py --steps 6 --warmup 2 --fp8 --fp8-gemm pp > $O/f8pp_$r.log 2>&1 || { tail -3 $O/f8pp_$r.log; exit 1; }
   echo "fp8 pp-all r=$r $(v $O/f8pp_$r.log)"
 done
+timeout -k 10 400 python bench.py --model llama_1b.json --steps 3 --warmup 1 > $O/b1b.log 2>&1 || { tail -3 $O/b1b.log; exit 1; }
+echo "1b bf16 $(v $O/b1b.log)"
+timeout -k 10 400 python bench.py --model llama_1b.json --steps 3 --warmup 1 --fp8 > $O/b1b_f8.log 2>&1 || { tail -3 $O/b1b_f8.log; exit 1; }
+echo "1b fp8 $(v $O/b1b_f8.log)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 3 --warmup 1 --fp8 > $O/prof.log 2>&1 || { tail -5 $O/prof.log; exit 1; }
 f=$(find $O/prof -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && python3 scripts/prof_summary.py $f > $O/kernel_stats.md; head -30 $O/kernel_stats.md
