@@ -1056,7 +1056,10 @@ __global__ void __launch_bounds__(256) attn_neg_stats_kernel(const float* __rest
 }
 
 // NW: waves per workgroup (8 = 256-key blocks: every Q / dO tile DMA'd once per 256 keys)
-template <int HD, bool ROPE_OUT, int BQ = 64, bool PAD = false, int NW = 4>
+// ABL (timing ablations, wrong results; ND_ATTN_DKDV_ABL): 1 no Q / dO / statistics DMA and no vmcnt wait,
+// 2 no barrier, 4 no softmax VALU (P = S, dS = dP), 8 no S / dP MFMAs, 16 no dV / dK MFMAs, 32 LDS fragments
+// read only in the first step
+template <int HD, bool ROPE_OUT, int BQ = 64, bool PAD = false, int NW = 4, int ABL = 0>
 __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ NL, const float* __restrict__ ND, bf16_t* __restrict__ dK,
@@ -1136,10 +1139,12 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
     }
   };
   issue(0);
+  bf16x8 qa[NT], da[NT], tdo[2][NO], tq[2][NO];
+  bool first = true;
   for (int it = 0; it < nit; ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of tile it has landed
-    __syncthreads();                                  // everyone's; and tile it-1's buffer is free
-    if (it + 1 < nit) issue(it + 1);
+    if constexpr (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of tile it has landed
+    if constexpr (!(ABL & 2)) __syncthreads();        // everyone's; and tile it-1's buffer is free
+    if constexpr (!(ABL & 1)) if (it + 1 < nit) issue(it + 1);
     const int q0 = qstart + (it % ntq) * BQ;
     const int buf = it & 1;
     const bf16_t* Qt = Qs + buf * (BQ * HD);
@@ -1153,11 +1158,14 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
       // All LDS fragments of this step are issued up front (row reads for S / dP, transposing reads
       // for dV / dK) so their latency hides behind the MFMA chains and the softmax VALU instead of
       // being exposed one s_waitcnt at a time.
-      bf16x8 qa[NT], da[NT];
+      const bool rd = !(ABL & 32) || first;
+      first = false;
+      if (rd) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        qa[t] = row_frag<HD>(Qt, qs * 32 + c32, t, h);
-        da[t] = row_frag<HD>(dOt, qs * 32 + c32, t, h);
+        for (int t = 0; t < NT; ++t) {
+          qa[t] = row_frag<HD>(Qt, qs * 32 + c32, t, h);
+          da[t] = row_frag<HD>(dOt, qs * 32 + c32, t, h);
+        }
       }
       f32x16 s, dp;  // seeded with -LSE / c and -delta of each query row
 #pragma unroll
@@ -1168,21 +1176,28 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
         s[4 * r4 + 0] = l4.x; s[4 * r4 + 1] = l4.y; s[4 * r4 + 2] = l4.z; s[4 * r4 + 3] = l4.w;
         dp[4 * r4 + 0] = d4.x; dp[4 * r4 + 1] = d4.y; dp[4 * r4 + 2] = d4.z; dp[4 * r4 + 3] = d4.w;
       }
-      bf16x8 tdo[2][NO], tq[2][NO];
+      if (rd) {
 #pragma unroll
-      for (int sidx = 0; sidx < 2; ++sidx)
+        for (int sidx = 0; sidx < 2; ++sidx)
 #pragma unroll
-        for (int o = 0; o < NO; ++o) {
-          tdo[sidx][o] = tr_frag<HD>(dOt, qs * 32 + 16 * sidx, o * 32, g, i16);
-          tq[sidx][o] = tr_frag<HD>(Qt, qs * 32 + 16 * sidx, o * 32, g, i16);
-        }
+          for (int o = 0; o < NO; ++o) {
+            tdo[sidx][o] = tr_frag<HD>(dOt, qs * 32 + 16 * sidx, o * 32, g, i16);
+            tq[sidx][o] = tr_frag<HD>(Qt, qs * 32 + 16 * sidx, o * 32, g, i16);
+          }
+      }
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        s = mfma32(qa[t], kf[t], s);
-        dp = mfma32(da[t], vf[t], dp);
+        if constexpr ((ABL & 8) != 0) {
+          s[t] += (float)qa[t][0];
+          dp[t] += (float)da[t][0];
+        } else {
+          s = mfma32(qa[t], kf[t], s);
+          dp = mfma32(da[t], vf[t], dp);
+        }
       }
       const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T) || (PAD && kw0 < ks);
-      if (!diag) {
+      if constexpr ((ABL & 4) != 0) {
+      } else if (!diag) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float p = fexp2(s[r] * c);
@@ -1204,12 +1219,18 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
         const bf16x8 dsf = pack_frag(dp, sidx);
 #pragma unroll
         for (int o = 0; o < NO; ++o) {
-          dv[o] = mfma32(tdo[sidx][o], pf, dv[o]);
-          dk[o] = mfma32(tq[sidx][o], dsf, dk[o]);
+          if constexpr ((ABL & 16) != 0) {
+            dv[o][sidx] += (float)pf[o] + (float)tdo[sidx][o][0];
+            dk[o][sidx] += (float)dsf[o] + (float)tq[sidx][o][0];
+          } else {
+            dv[o] = mfma32(tdo[sidx][o], pf, dv[o]);
+            dk[o] = mfma32(tq[sidx][o], dsf, dk[o]);
+          }
         }
       }
     }
   }
+  if constexpr ((ABL & 1) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (key < T) {
     store_T<HD>(dK + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dk, scale, h, ROPE_OUT ? cosT : nullptr, sinT, key);
     store_T<HD>(dV + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dv, 1.f, h, nullptr, nullptr, 0);
@@ -1324,11 +1345,21 @@ static int bwd_fused_launch(const void* q, const void* k, const void* v, const v
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD, 8>), dim3((T + 255) / 256 * B * nkv), dim3(512),
                        0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
                        (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
-  else if (T % 128 == 0)
-    hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
-                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
-                       (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
-  else
+  else if (T % 128 == 0) {
+    const char* ab = getenv("ND_ATTN_DKDV_ABL");  // timing ablations (wrong results)
+    const int abl = ab ? atoi(ab) : 0;
+    switch (abl) {
+#define ND_DA(X) case X: hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD, 4, X>), dim3(nb * B * nkv), \
+      dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd, (bf16_t*)dk, \
+      (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv)); break;
+      ND_DA(1) ND_DA(2) ND_DA(3) ND_DA(4) ND_DA(8) ND_DA(16) ND_DA(24) ND_DA(32) ND_DA(28) ND_DA(63)
+#undef ND_DA
+      default:
+        hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
+                           (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
+                           (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
+    }
+  } else
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 64, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
                        (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
