@@ -30,6 +30,15 @@ from .. import ops
 from ..config import LlamaConfig
 from .param_store import ParamStore
 
+_WARNED = set()
+
+
+def _warn_once(key: str, msg: str) -> None:
+    if key not in _WARNED:
+        _WARNED.add(key)
+        import warnings
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
+
 
 @dataclasses.dataclass
 class CausalLMOutput:
@@ -206,6 +215,10 @@ class LlamaForCausalLM:
                                 c.head_dim, rope_cols)
             rotated = True
         else:
+            if self.fp8 is not None and not fp8_qkv:
+                _warn_once("qkv", "--fp8-keep-fused rope: the fused bf16 q|k|v + RoPE GEMM cannot run on this "
+                                  "shape; the projection runs as a plain bf16 GEMM + separate RoPE pass (slower "
+                                  "than fp8)")
             qkv = self._linear(f"{i}.qkv", y, w_qkv, self._fused(qn, "grad"), y8)
             rotated = False
         o = ops.attention(qkv, cos, sin, B, T, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
@@ -225,6 +238,9 @@ class LlamaForCausalLM:
                 m = ops.mlp_fused(y, w_gu, self._fused(gn, "grad"), wt_gu, w_dn,
                                   self._g(p + "mlp.down_proj.weight"), wt_dn)
                 return m, h
+            if self.fp8 is not None:
+                _warn_once("mlp", "--fp8-keep-fused mlp: the fused bf16 SwiGLU GEMMs cannot run on this shape; "
+                                  "the MLP runs as plain bf16 GEMMs + separate SwiGLU passes (slower than fp8)")
         elif self.fp8.mlp_ok(y, w_gu, w_dn):
             # the same fusion on the own fp8 GEMMs
             m = self.fp8.mlp(f"{i}.gu", f"{i}.down", y, w_gu, w_dn, self._fused(gn, "grad"),
