@@ -84,10 +84,10 @@ def parse():
     ap.add_argument("--fp8-wgrad", type=int, default=1, choices=[0, 1],
                     help="with --fp8: weight-gradient GEMMs in fp8 too (own kernel on the token-major fp8 "
                          "operands; default on)")
-    ap.add_argument("--fp8-gemm", default="auto", choices=["auto", "pp", "hip", "hipblaslt"],
-                    help="with --fp8: forward / input-gradient fp8 GEMMs: auto (default: own fp8 ping-pong kernel "
-                         "with the fused epilogues, hipBLASLt for the long-K N<=1024 plain products), pp (own "
-                         "kernel for all), hip (round-2 fp8 kernel) or hipblaslt")
+    ap.add_argument("--fp8-gemm", default="pp", choices=["pp", "auto", "hip", "hipblaslt"],
+                    help="with --fp8: forward / input-gradient fp8 GEMMs: pp (default: the own fp8 ping-pong kernel "
+                         "with the fused epilogues for every product), auto (hipBLASLt for the long-K N<=1024 plain "
+                         "products), hip (round-2 fp8 kernel) or hipblaslt")
     ap.add_argument("--fp8-fused-epi", type=int, default=1, choices=[0, 1],
                     help="with --fp8 and --fp8-gemm pp: RoPE / SwiGLU fused into the fp8 GEMM epilogues")
     ap.add_argument("--fp8-keep-fused", default="none", choices=["none", "rope", "mlp", "both"],

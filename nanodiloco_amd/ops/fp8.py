@@ -48,16 +48,16 @@ _FUSED = {"enabled": True}
 # also carries the fused RoPE / SwiGLU epilogues; "hip": the round-2 one-wave-per-SIMD fp8 kernel
 # (csrc/gemm_f8.hip); "hipblaslt": torch._scaled_mm.  Shapes the own kernels do not take fall back to
 # torch._scaled_mm.
-_GEMM = {"backend": "auto"}
+_GEMM = {"backend": "pp"}
 # fp8 projections with their fused epilogues on the own fp8 GEMM: q|k|v + RoPE, gate|up + SwiGLU and the
 # down input gradient + SwiGLU backward (backend "pp" only)
 _EPI = {"enabled": True}
 
 
 def set_fp8_gemm(backend: str) -> None:
-    """fp8 forward / input-gradient GEMMs: "auto" (default: the own fp8 kernel for the fused-epilogue
-    products and every plain product it matches, hipBLASLt for the long-K N <= 1024 plain products),
-    "pp" (the own kernel for everything), "hip" or "hipblaslt"."""
+    """fp8 forward / input-gradient GEMMs: "pp" (default: the own fp8 ping-pong kernel for every product),
+    "auto" (hipBLASLt for the three long-K N <= 1024 plain products, where the own kernel runs 0.8x;
+    +0.2 % per step, within noise: profiles/r4_fp8_pp.md), "hip" (round-2 kernel) or "hipblaslt"."""
     if backend not in ("auto", "pp", "hip", "hipblaslt"):
         raise ValueError(backend)
     _GEMM["backend"] = backend

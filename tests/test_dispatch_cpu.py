@@ -10,10 +10,10 @@ from nanodiloco_amd.ops import gemm as G
 
 def test_fp8_gemm_backend_switch():
     old = fp8.fp8_gemm_backend()
-    assert old == "auto"  # own fp8 ping-pong kernel + fused epilogues, hipBLASLt for long-K narrow plain products
+    assert old == "pp"  # own fp8 ping-pong kernel + fused epilogues for every product (profiles/r4_fp8_pp.md)
     assert fp8.fp8_fused_epilogues()
     try:
-        fp8.set_fp8_gemm("pp")
+        fp8.set_fp8_gemm("auto")
         assert fp8.fp8_fused_epilogues()
         fp8.set_fp8_gemm("hip")
         assert fp8.fp8_gemm_backend() == "hip"
