@@ -43,6 +43,22 @@ def main():
     for nm, (m, n) in shapes.items():
         dy, x, gw = r(M, m), r(M, n), torch.zeros(m, n, device="cuda")
         cases[nm] = (2.0 * M * m * n, dy, x, gw)
+    # correct variants (64: half the pieces issued inside the MFMA phase) must match the default bitwise
+    for nm, (fl, dy, x, gw) in cases.items():
+        for arm in arms:
+            if arm not in ("a64",):
+                continue
+            outs = []
+            for v in ("", arm):
+                if v:
+                    os.environ["ND_WGRAD_VARIANT"] = v
+                else:
+                    os.environ.pop("ND_WGRAD_VARIANT", None)
+                gw.zero_()
+                G.wgrad(gw, dy, x)
+                outs.append(gw.clone())
+            os.environ.pop("ND_WGRAD_VARIANT", None)
+            print(f"check {nm} {arm}: bitwise equal to the default: {torch.equal(outs[0], outs[1])}", flush=True)
     res = {}
     for _ in range(a.rounds):
         for nm, (fl, dy, x, gw) in cases.items():
