@@ -37,6 +37,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=131072)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--pp-variant", type=int, default=1024, help="gemm_pp variant of the B arm (1024: buffer form)")
+    ap.add_argument("--wgrad-variant", default="b", help="ND_WGRAD_VARIANT of the B arm (b: buffer form)")
     a = ap.parse_args()
     ops.set_backend("hip")
     M, d, F, V = a.tokens, 1024, 2688, 32000
@@ -60,13 +62,14 @@ def main():
     }
 
     def arm(name, flat):
+        """flat: the default build; else the B arm (--pp-variant / --wgrad-variant)"""
         if name.startswith("wgrad"):
             if flat:
                 os.environ.pop("ND_WGRAD_VARIANT", None)
             else:
-                os.environ["ND_WGRAD_VARIANT"] = "b"
+                os.environ["ND_WGRAD_VARIANT"] = a.wgrad_variant
         else:
-            G.set_pp_variant(0 if flat else 1024)
+            G.set_pp_variant(0 if flat else a.pp_variant)
 
     bad = 0
     for name, (fl, fn) in cases.items():
@@ -86,7 +89,7 @@ def main():
             outs.append(o.float().clone())
         same = torch.equal(outs[0], outs[1])
         bad += not same
-        print(f"check {name}: flat == buffer bitwise: {same}", flush=True)
+        print(f"check {name}: default == variant bitwise: {same}", flush=True)
     res = {}
     for rd in range(a.rounds):
         for name, (fl, fn) in cases.items():
@@ -100,9 +103,9 @@ def main():
         t = [sorted(res[(name, f)])[a.rounds // 2] for f in (False, True)]
         tot[0] += t[0]
         tot[1] += t[1]
-        print(f"{name:20s} | buffer {t[0]:8.1f} us {fl / t[0] / 1e6:5.0f} TF | flat {t[1]:8.1f} us "
-              f"{fl / t[1] / 1e6:5.0f} TF | {t[0] / t[1]:.3f}x", flush=True)
-    print(f"total buffer {tot[0]:.0f} us flat {tot[1]:.0f} us ({tot[0] / tot[1]:.3f}x)", flush=True)
+        print(f"{name:20s} | variant {t[0]:8.1f} us {fl / t[0] / 1e6:5.0f} TF | default {t[1]:8.1f} us "
+              f"{fl / t[1] / 1e6:5.0f} TF | default/variant speed {t[0] / t[1]:.3f}x", flush=True)
+    print(f"total variant {tot[0]:.0f} us default {tot[1]:.0f} us ({tot[0] / tot[1]:.3f}x)", flush=True)
     sys.exit(1 if bad else 0)
 
 
