@@ -565,28 +565,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
     }
   };
 
-  // single pieces (SPLIT, ABL 4096: half of each K-tile's pieces issued inside the MFMA phase, where a piece
-  // costs ~60 cycles instead of the 100-185 it costs in a LOAD phase that also carries the fragment reads)
-  constexpr bool SPLIT = (ABL & 4096) != 0;
-  auto piece_b = [&](const Pos& p, int s, int h, int q) __attribute__((always_inline)) {
-    const uint32_t dst = lds0 + (uint32_t)(s & 1) * BUF_B + 2 * HALF_B + (uint32_t)wn * 1024u + (uint32_t)h * HALF_B +
-                         (uint32_t)q * 4096u;
-    const bool full = EPI == PP_SWIGLU ? p.n0 + 128 <= N : p.n0 + 128 * h + 128 <= N;
-    if (!(ABL & 1024) && full) {
-      gdma(B + ((int64_t)(p.n0 + (EPI == PP_SWIGLU ? 64 : 128) * h) * ldb + (int64_t)p.kt * TKE) * ES, voff[q], dst);
-    } else {
-      dma(b_rsrc(p.n0, p.kt, h), voff[q], dst);
-    }
-  };
-  auto piece_a = [&](const Pos& p, int s, int h, int q) __attribute__((always_inline)) {
-    const uint32_t dst = lds0 + (uint32_t)(s & 1) * BUF_B + (uint32_t)h * HALF_B + (uint32_t)wn * 1024u + (uint32_t)q * 4096u;
-    if (!(ABL & 1024) && p.m0 + 128 * h + 128 <= M) {
-      gdma(A + ((int64_t)(p.m0 + 128 * h) * lda + (int64_t)p.kt * TKE) * ES, voff[q], dst);
-    } else {
-      dma(a_rsrc(p.m0, p.kt, h), voff[q], dst);
-    }
-  };
-
   // ---- fragment reads: A rows 16 a + (lane & 15) of half g, B rows (wn & 1) 64 + 16 b + (lane & 15) of
   // half 2 + (wn >> 1); chunk (4 ks + lane / 16) ^ swizzle -- the same per-lane offset for A and B
   const int r16 = lane & 15, q = lane >> 4;
@@ -649,20 +627,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
       if (ABL & 1) {
       } else if (g == 0) {
         if (more1) {
-          if constexpr (SPLIT) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) piece_b(pb, s + 1, 0, q);  // half 1: in COMPUTE(s)
-          } else {
-            stage_b(pb, s + 1);
-            pos_next(pb);
-          }
+          stage_b(pb, s + 1);
+          pos_next(pb);
         }
       } else {
         if (more1) {
           stage_a(pa1, s + 1, 1);
           pos_next(pa1);
         }
-        if (!SPLIT && more2) {  // SPLIT: A0(s + 2) in COMPUTE(s)
+        if (more2) {
           stage_a(pa0, s + 2, 0);
           pos_next(pa0);
         }
@@ -699,27 +672,11 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
     }
     if (!reads_first && (!(ABL & 2) || F)) load_frags(s);
     __builtin_amdgcn_s_waitcnt(LGKM0);
-    if (g == 1 && !(ABL & 16)) {  // A0(s + 1) landed
-      if constexpr (SPLIT) vmwait_n<NST>((more1 ? 4 : 0) + (fat ? NST : 0));  // A0(s + 1) came in COMPUTE(s - 1)
-      else vmwait_n<NST>((more1 ? 4 : 0) + (more2 ? 4 : 0) + (fat || after_fat ? NST : 0));
-    }
+    if (g == 1 && !(ABL & 16))
+      vmwait_n<NST>((more1 ? 4 : 0) + (more2 ? 4 : 0) + (fat || after_fat ? NST : 0));  // A0(s + 1) landed
     if (!(ABL & 4)) bar();
     // ================= COMPUTE(s)
     __builtin_amdgcn_s_setprio(1);
-    // SPLIT: the other half's pieces after MFMAs 2, 10, 18, 26 of the phase
-    auto split_piece = [&](int i) __attribute__((always_inline)) {
-      if constexpr (SPLIT && !(ABL & 1)) {
-        if ((i & 7) == 2 && i < 32) {
-          __builtin_amdgcn_sched_barrier(0);
-          if (g == 0) {
-            if (more1) piece_b(pb, s + 1, 1, i >> 3);
-          } else {
-            if (more2) piece_a(pa0, s + 2, 0, i >> 3);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    };
     if constexpr (F8 != 0) {
 #pragma unroll
       for (int a = 0; a < 8; ++a)
@@ -727,7 +684,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
         for (int b = 0; b < 4; ++b) {
           if constexpr (F) mma8z<F8>(cat16(fb[b][0], fb[b][1]), cat16(fa[a][0], fa[a][1]), acc[a][b], one);
           else mma8<F8>(cat16(fb[b][0], fb[b][1]), cat16(fa[a][0], fa[a][1]), acc[a][b], one);
-          split_piece(a * 4 + b);
         }
     } else {
 #pragma unroll
@@ -736,7 +692,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
       for (int b = 0; b < 4; ++b) {
         if constexpr (F) mma0(fb[b][0], fa[a][0], acc[a][b]);
         else mma(fb[b][0], fa[a][0], acc[a][b]);
-        split_piece(a * 4 + b);
       }
 #pragma unroll
     for (int a = 0; a < 8; ++a)
@@ -744,17 +699,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
       for (int b = 0; b < 4; ++b) mma(fb[b][1], fa[a][1], acc[a][b]);
     }
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (SPLIT && !(ABL & 1)) {  // the positions the COMPUTE-phase pieces used move on now
-      if (g == 0) {
-        if (more1) pos_next(pb);
-      } else {
-        if (more2) pos_next(pa0);
-      }
-    }
     if (ABL & 16) {
     } else if (g == 0) {
-      if constexpr (SPLIT) vmwait<0>();  // B(s + 1) landed: its last pieces are the youngest
-      else vmwait_n<NST>(fat ? NST : 0);  // B(s + 1) landed
+      vmwait_n<NST>(fat ? NST : 0);  // B(s + 1) landed
     } else {
       vmwait_n<NST>((more2 ? 4 : 0) + (fat ? NST : 0));  // A1(s + 1) landed
     }
@@ -819,7 +766,6 @@ template <int EPI, int HD = 64>
 int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
               const PPEpi& ep, hipStream_t s) {
   if (g_pp_variant == 1024) return launch_pp_v<EPI, HD, 1024>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
-  if (g_pp_variant == 4096) return launch_pp_v<EPI, HD, 4096>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
   if constexpr (EPI == PP_STORE) {
     switch (g_pp_variant) {
       case 1: return launch_pp_v<EPI, HD, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);

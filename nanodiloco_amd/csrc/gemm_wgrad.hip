@@ -730,21 +730,6 @@ __global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restri
       for (int q = 0; q < 4; ++q) wpp_dma(r, voff[q], dst + (uint32_t)q * 4096u);
     }
   };
-  // one piece (q) of half h of K-tile kt: the SPLIT variant issues half of each K-tile's pieces inside the
-  // MFMA phase, where a piece costs ~60 cycles instead of the 100-185 it costs in a LOAD phase that also
-  // carries the fragment reads (MI355X_MICROARCH: LDS-DMA piece issue cost)
-  auto stage_piece = [&](int kt, int h, int q) __attribute__((always_inline)) {
-    const int64_t e0 = (int64_t)(kbeg + 64 * kt) * ld + (g == 0 ? n0 : m0) + 128 * h;
-    const uint32_t dst = lds0 + (uint32_t)(kt & 1) * WPP_BUF_B + (uint32_t)(g == 0 ? 2 + h : h) * WPP_HALF_B +
-                         (uint32_t)wn * 1024u + (uint32_t)q * 4096u;
-    if (GD && (g == 0 ? n0 + 128 * h + 128 <= N : m0 + 128 * h + 128 <= M)) {
-      wpp_gdma((g == 0 ? B : A) + e0, voff[q], dst);
-    } else {
-      const auto r = wpp_rsrc((g == 0 ? B : A) + e0, ((int64_t)K * ld - e0) * 2);
-      wpp_dma(r, voff[q], dst);
-    }
-  };
-  constexpr bool SPLIT = (ABL & 64) != 0;
   bf16x8 fa[8][2], fb[4][2];
   auto load_frags = [&](int kt) __attribute__((always_inline)) {
     const char* base = smem + (kt & 1) * WPP_BUF_B;
@@ -783,15 +768,15 @@ __global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restri
     } else if (g == 0) {
       if (more1) {
         stage(s + 1, 0);
-        if (!SPLIT) stage(s + 1, 1);
+        stage(s + 1, 1);
       }
     } else {
-      if (more1) stage(s + 1, 1);               // A1(s + 1)
-      if (!SPLIT && more2) stage(s + 2, 0);     // A0(s + 2)
+      if (more1) stage(s + 1, 1);  // A1(s + 1)
+      if (more2) stage(s + 2, 0);  // A0(s + 2)
     }
     if (!(ABL & 2) || s == 0) load_frags(s);
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    if (g == 1 && !(ABL & 8)) wpp_vmn((more1 ? 4 : 0) + (!SPLIT && more2 ? 4 : 0));  // A0(s + 1) landed
+    if (g == 1 && !(ABL & 8)) wpp_vmn((more1 ? 4 : 0) + (more2 ? 4 : 0));  // A0(s + 1) landed
     if (!(ABL & 4)) wpp_bar();
     // ================= COMPUTE(s)
     __builtin_amdgcn_s_setprio(1);
@@ -806,21 +791,7 @@ __global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restri
 #pragma unroll
       for (int a = 0; a < 8; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          acc[a][b] = wpp_mma(fa[a][ks], fb[b][ks], acc[a][b]);
-          if constexpr (SPLIT) {
-            const int i = ks * 32 + a * 4 + b;
-            if ((i & 7) == 2 && i < 32) {  // after MFMAs 2, 10, 18, 26: the other half's pieces
-              __builtin_amdgcn_sched_barrier(0);
-              if (g == 0) {
-                if (more1) stage_piece(s + 1, 1, i >> 3);
-              } else {
-                if (more2) stage_piece(s + 2, 0, i >> 3);
-              }
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          }
-        }
+        for (int b = 0; b < 4; ++b) acc[a][b] = wpp_mma(fa[a][ks], fb[b][ks], acc[a][b]);
     }
     __builtin_amdgcn_s_setprio(0);
     if (ABL & 8) {
@@ -1120,7 +1091,7 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
   hipLaunchKernelGGL((wgrad_pp_kernel<true, X>), dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, \
                      (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk); break;
-      switch (abl) { ND_WA(1) ND_WA(2) ND_WA(4) ND_WA(8) ND_WA(16) ND_WA(3) ND_WA(7) ND_WA(15) ND_WA(31) ND_WA(64) default: return (int)hipErrorInvalidValue; }
+      switch (abl) { ND_WA(1) ND_WA(2) ND_WA(4) ND_WA(8) ND_WA(16) ND_WA(3) ND_WA(7) ND_WA(15) ND_WA(31) default: return (int)hipErrorInvalidValue; }
 #undef ND_WA
       ND_LAUNCH_CHECK();
     }
