@@ -1237,205 +1237,6 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// dK / dV, software-pipelined for ONE wave per SIMD (round 4, ND_ATTN_DKDV=sp; HD = 64, 128-query tiles).
-// The two-waves-per-SIMD kernel above is a latency chain (profiles/r4_attention_dkdv_ablation.md):
-// per 32-query step, LDS reads -> S / dP MFMAs -> exp, P.dP -> pack -> dV / dK MFMAs, with only the
-// partner wave to overlap.  Here each wave has the whole 512-register file and keeps two steps in
-// flight: the S / dP MFMAs of step i + 1 are issued between the softmax instructions of step i (the
-// MFMA pipe and the VALU run side by side, ~5 single-issue instructions hide per 32x32x16 gap), then
-// the dV / dK MFMAs of step i.  Every step of a tile is computed (causally skipped steps of the
-// diagonal tile run masked: P = 0), so the pipeline has no data-dependent holes.
-template <int HD, bool ROPE_OUT, bool PAD = false>
-__global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_sp_kernel(
-    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-    const bf16_t* __restrict__ dO, const float* __restrict__ NL, const float* __restrict__ ND, bf16_t* __restrict__ dK,
-    bf16_t* __restrict__ dV, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
-    const float* __restrict__ cosT, const float* __restrict__ sinT, const int* __restrict__ KS, int order) {
-  constexpr int BQ = 128, NW = 4;
-  constexpr int NT = HD / 16, NO = HD / 32;
-  constexpr int CPR = HD / 8;
-  constexpr int RPI = 64 / CPR;
-  constexpr int IPW = (BQ / RPI) / NW;
-  constexpr int KB = 32 * NW;
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[2 * BQ * HD];
-  __shared__ __attribute__((aligned(16))) bf16_t dOs[2 * BQ * HD];
-  __shared__ __attribute__((aligned(16))) float lse_s[2 * BQ];
-  __shared__ __attribute__((aligned(16))) float del_s[2 * BQ];
-
-  const int bk_count = B * nkv, rep = nh / nkv, nkb = (T + KB - 1) / KB;
-  int kb, bk;
-  if (order) {
-    const int id = xcd_remap(blockIdx.x, nkb * bk_count);
-    bk = id / nkb;
-    kb = id % nkb;
-  } else {
-    kb = (int)(blockIdx.x / bk_count);
-    bk = blockIdx.x % bk_count;
-  }
-  const int b = bk / nkv, kvh = bk % nkv;
-  const int ks = PAD ? KS[b] : 0;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int g = lane >> 4, i16 = lane & 15;
-  const int kw0 = kb * KB + w * 32, key = kw0 + c32;
-  const float c = scale * LOG2E;
-  const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
-  const bf16_t* Vb = V + (int64_t)b * T * ld + (int64_t)kvh * HD;
-
-  bf16x8 kf[NT], vf[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    kf[t] = key < T ? load16(Kb + (int64_t)key * ld + 16 * t + 8 * h) : zero8();
-    vf[t] = key < T ? load16(Vb + (int64_t)key * ld + 16 * t + 8 * h) : zero8();
-  }
-  f32x16 dk[NO], dv[NO];
-#pragma unroll
-  for (int o = 0; o < NO; ++o) { dk[o] = f32x16{}; dv[o] = f32x16{}; }
-
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  uint32_t vq[IPW], vd[IPW];
-#pragma unroll
-  for (int i = 0; i < IPW; ++i) {
-    const int row = (wu + NW * i) * RPI + lane / CPR, p = lane % CPR;
-    const int lch = (soff<HD>(row, p * 8) - row * HD) / 8;
-    vq[i] = (uint32_t)(((int64_t)row * ld + lch * 8) * 2);
-    vd[i] = (uint32_t)(((int64_t)row * ldo + lch * 8) * 2);
-  }
-  const uint32_t qs_a = lds_addr(Qs), do_a = lds_addr(dOs), ls_a = lds_addr(lse_s), ds_a = lds_addr(del_s);
-  const int qstart = (kb * KB) / BQ * BQ;
-  const int ntq = (T - qstart + BQ - 1) / BQ;
-  const int nit = ntq * rep;
-  auto issue = [&](int it) {
-    const int head = kvh * rep + it / ntq;
-    const int q0 = qstart + (it % ntq) * BQ;
-    const int buf = it & 1;
-    const bf16_t* sq = Q + ((int64_t)b * T + q0) * ld + (int64_t)head * HD;
-    const bf16_t* sd = dO + ((int64_t)b * T + q0) * ldo + (int64_t)head * HD;
-#pragma unroll
-    for (int i = 0; i < IPW; ++i) {
-      const uint32_t off = (uint32_t)(buf * BQ * HD * 2 + (wu + NW * i) * 1024);
-      adma_b128(sq, vq[i], qs_a + off);
-      adma_b128(sd, vd[i], do_a + off);
-    }
-    if (wu < BQ / 64) {
-      const int64_t rs = ((int64_t)b * nh + head) * T + q0 + wu * 64;
-      adma_b32(NL + rs, (uint32_t)(lane * 4), ls_a + (buf * BQ + wu * 64) * 4);
-      adma_b32(ND + rs, (uint32_t)(lane * 4), ds_a + (buf * BQ + wu * 64) * 4);
-    }
-  };
-
-  // one 32-query step's state
-  struct St {
-    bf16x8 qa[NT], da[NT], tdo[2][NO], tq[2][NO];
-    f32x16 s, dp;
-  };
-  St X, Y;
-  // R: every LDS read of step qs of the current tile (row fragments, transposed fragments, statistics)
-  auto R = [&](St& st, const bf16_t* Qt, const bf16_t* dOt, const float* lt, const float* dt, int qs)
-      __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      st.qa[t] = row_frag<HD>(Qt, qs * 32 + c32, t, h);
-      st.da[t] = row_frag<HD>(dOt, qs * 32 + c32, t, h);
-    }
-#pragma unroll
-    for (int r4 = 0; r4 < 4; ++r4) {
-      const int qr = qs * 32 + 8 * r4 + 4 * h;
-      const float4 l4 = *reinterpret_cast<const float4*>(lt + qr);
-      const float4 d4 = *reinterpret_cast<const float4*>(dt + qr);
-      st.s[4 * r4 + 0] = l4.x; st.s[4 * r4 + 1] = l4.y; st.s[4 * r4 + 2] = l4.z; st.s[4 * r4 + 3] = l4.w;
-      st.dp[4 * r4 + 0] = d4.x; st.dp[4 * r4 + 1] = d4.y; st.dp[4 * r4 + 2] = d4.z; st.dp[4 * r4 + 3] = d4.w;
-    }
-#pragma unroll
-    for (int sidx = 0; sidx < 2; ++sidx)
-#pragma unroll
-      for (int o = 0; o < NO; ++o) {
-        st.tdo[sidx][o] = tr_frag<HD>(dOt, qs * 32 + 16 * sidx, o * 32, g, i16);
-        st.tq[sidx][o] = tr_frag<HD>(Qt, qs * 32 + 16 * sidx, o * 32, g, i16);
-      }
-  };
-  // A(next) interleaved with B(cur): S / dP MFMA t of the next step, then a quarter of the current
-  // step's softmax (4 of its 16 score registers)
-  // MASK: the diagonal / tail / left-pad tile needs the per-score visibility test; every other step
-  // computes exp unconditionally (a lane-varying ?: around the exp becomes one branch per score)
-  auto softmax_part = [&](auto MASK, St& st, int qsub, int t) __attribute__((always_inline)) {
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int r = 4 * t + rr;
-      float p = fexp2(st.s[r] * c);
-      if constexpr (decltype(MASK)::value) {
-        const int qq = qsub + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const bool vis = key <= qq && qq < T && key < T && (!PAD || key >= ks);
-        p = vis ? p : 0.f;
-      }
-      st.s[r] = p;
-      st.dp[r] = p * st.dp[r];
-    }
-  };
-  auto mma_sdp = [&](St& st, int t) __attribute__((always_inline)) {
-    st.s = mfma32(st.qa[t], kf[t], st.s);
-    st.dp = mfma32(st.da[t], vf[t], st.dp);
-  };
-  auto mma_kv = [&](St& st) __attribute__((always_inline)) {
-#pragma unroll
-    for (int sidx = 0; sidx < 2; ++sidx) {
-      const bf16x8 pf = pack_frag(st.s, sidx);
-      const bf16x8 dsf = pack_frag(st.dp, sidx);
-#pragma unroll
-      for (int o = 0; o < NO; ++o) {
-        dv[o] = mfma32(st.tdo[sidx][o], pf, dv[o]);
-        dk[o] = mfma32(st.tq[sidx][o], dsf, dk[o]);
-      }
-    }
-  };
-  // B(cur) + A(next) interleaved, then C(cur)
-  auto step = [&](St& cur, St& nxt, int qsub_cur, bool has_next) __attribute__((always_inline)) {
-    const bool diag = (kw0 + 31 > qsub_cur) || (qsub_cur + 31 >= T) || (key >= T) || (PAD && kw0 < ks);
-    if (diag) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        if (has_next) mma_sdp(nxt, t);
-        softmax_part(std::true_type{}, cur, qsub_cur, t);
-      }
-    } else {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        if (has_next) mma_sdp(nxt, t);
-        softmax_part(std::false_type{}, cur, qsub_cur, t);
-      }
-    }
-    mma_kv(cur);
-  };
-
-  issue(0);
-  for (int it = 0; it < nit; ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (it + 1 < nit) issue(it + 1);
-    const int q0 = qstart + (it % ntq) * BQ;
-    const int buf = it & 1;
-    const bf16_t* Qt = Qs + buf * (BQ * HD);
-    const bf16_t* dOt = dOs + buf * (BQ * HD);
-    const float* lt = lse_s + buf * BQ;
-    const float* dt = del_s + buf * BQ;
-    if (kw0 >= T || kw0 > q0 + BQ - 1) continue;  // wave-uniform: the whole tile is before our keys
-    R(X, Qt, dOt, lt, dt, 0);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) mma_sdp(X, t);
-    R(Y, Qt, dOt, lt, dt, 1);
-    step(X, Y, q0, true);
-    R(X, Qt, dOt, lt, dt, 2);
-    step(Y, X, q0 + 32, true);
-    R(Y, Qt, dOt, lt, dt, 3);
-    step(X, Y, q0 + 64, true);
-    step(Y, X, q0 + 96, false);
-  }
-  if (key < T) {
-    store_T<HD>(dK + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dk, scale, h, ROPE_OUT ? cosT : nullptr, sinT, key);
-    store_T<HD>(dV + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dv, 1.f, h, nullptr, nullptr, 0);
-  }
-}
-
 template <int HD, bool ROPE, bool ROPE_OUT, bool PAD>
 static void bwd_launch_t(const void* q, const void* k, const void* v, const void* dout, const float* lse,
                          const float* delta, void* dq, void* dk, void* dv, float* ws, int B, int nh, int nkv, int T,
@@ -1538,20 +1339,9 @@ static int bwd_fused_launch(const void* q, const void* k, const void* v, const v
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
                        (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks, attn_order());
   const char* kwe = getenv("ND_ATTN_DKDV_W");
-  const char* spe = getenv("ND_ATTN_DKDV");
   bool kw8 = false;
   if constexpr (HD >= 64) kw8 = kwe && kwe[0] == '8' && T % 128 == 0;
-  bool sp = false;
-  if constexpr (HD == 64) {
-    if (spe && spe[0] == 's' && T % 128 == 0) {  // software-pipelined, one wave per SIMD (A/B)
-      hipLaunchKernelGGL((attn_bwd_dkdv_sp_kernel<HD, ROPE_OUT, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
-                         (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
-                         (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
-      sp = true;
-    }
-  }
-  if (sp) {
-  } else if (kw8)  // 256-key blocks
+  if (kw8)  // 256-key blocks
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD, 8>), dim3((T + 255) / 256 * B * nkv), dim3(512),
                        0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
                        (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
