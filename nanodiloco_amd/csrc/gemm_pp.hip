@@ -34,9 +34,11 @@
 //   group 1, LOAD(s): A1 of K-tile s+1, then A0 of K-tile s+2 (4 + 4 pieces / wave; A1(s+1) retired
 //                     at the end of its COMPUTE(s), A0(s+2) at the end of its LOAD(s+1))
 //
-// The waits are counted (`s_waitcnt vmcnt(N)`, never a drain of the whole stream), and the pieces go
-// through buffer descriptors whose record count ends at the operand's last row, so the M / N tail
-// rows read as out-of-range (no clamping, tile-independent per-lane offsets).
+// The waits are counted (`s_waitcnt vmcnt(N)`, never a drain of the whole stream).  Half-tiles whose rows
+// all exist are staged with FLAT-global LDS loads (`global_load_lds_dwordx4`, SGPR base + per-lane offset;
+// round 4, 1.004-1.011x); tail half-tiles go through buffer descriptors whose record count ends at the
+// operand's last row, so the M / N tail rows read as out-of-range (no clamping, tile-independent per-lane
+// offsets).
 //
 // Persistent: one workgroup per CU walks tiles first, first + G, ... (XCD-remapped; GM m-panels per
 // group of tiles so one XCD's 32 concurrent tiles share A / B panels in its L2), and the K-tile
@@ -52,6 +54,11 @@
 //               then the 32 matching up rows of the weight): stores gu = [gate | up] AND
 //               act = silu(gate) * up
 //   PP_DSWIGLU  down-projection input gradient: acc = d(act); reads gate / up, stores d(gate | up)
+//
+// fp8 operands (round 4, template F8): the same kernel with a 128-element fp8 K-tile (the same 128-B LDS
+// rows), one v_mfma_scale_f32_16x16x128_f8f6f4 per fragment pair, every epilogue on acc * sa * sb; the Q
+// forms of the SwiGLU epilogues write the e4m3 act / e5m2 d(gate|up) instead of the bf16 tensors
+// (profiles/r4_fp8_pp.md).
 //
 // Reference role: every nn.Linear of HF LlamaForCausalLM (/root/reference/nanodiloco/main.py:97-99,
 // run at :109-111).
