@@ -137,6 +137,27 @@ __device__ __forceinline__ void fp8_put8(const Fp8Out& f, int64_t off, const flo
   *reinterpret_cast<uint2*>(f.q + off) = o;
 }
 
+// bf16 store of 8 values and their fp8 side output from the SAME packed bf16 words: the rounded values
+// are unpacked (one shift / and each) instead of rounded a second time.  sc: the side output's scale,
+// read once per kernel by the caller.  Bitwise Vec8<BF16>::store + round_bf16x8 + fp8_put8.
+template <int FMT>
+__device__ __forceinline__ void put8_bf16_q_t(void* y, int64_t i, const float* v, uint8_t* q, float sc, float& amax) {
+  uint4 a;
+  a.x = pack2(v[0], v[1]); a.y = pack2(v[2], v[3]); a.z = pack2(v[4], v[5]); a.w = pack2(v[6], v[7]);
+  *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(y) + i) = a;
+  const float r[8] = {lo_bf(a.x), hi_bf(a.x), lo_bf(a.y), hi_bf(a.y), lo_bf(a.z), hi_bf(a.z), lo_bf(a.w), hi_bf(a.w)};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(r[j]));
+  uint2 o;
+  o.x = cvt4<FMT>(r[0] * sc, r[1] * sc, r[2] * sc, r[3] * sc);
+  o.y = cvt4<FMT>(r[4] * sc, r[5] * sc, r[6] * sc, r[7] * sc);
+  *reinterpret_cast<uint2*>(q + i) = o;
+}
+__device__ __forceinline__ void put8_bf16_q(void* y, int64_t i, const float* v, const Fp8Out& f, float sc, float& amax) {
+  if (f.fmt == 0) put8_bf16_q_t<0>(y, i, v, f.q, sc, amax);
+  else put8_bf16_q_t<1>(y, i, v, f.q, sc, amax);
+}
+
 __device__ __forceinline__ void round_bf16x8(float* v) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j]));

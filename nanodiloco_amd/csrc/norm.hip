@@ -19,6 +19,7 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const void* __restrict
                                                           float* __restrict__ h_out, float* __restrict__ rstd_out,
                                                           int64_t rows, int cols, float eps, Fp8Out q8) {
   float qmax = 0.f;
+  const float qsc = Q ? q8.scale[0] : 1.f;
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * 4;
@@ -53,11 +54,8 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const void* __restrict
         Vec8<F32>::load(w, col, wv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = wv[j] * (v[c][j] * rs);
-        Vec8<YDT>::store(y, base + col, o);
-        if (Q) {
-          round_bf16x8(o);
-          fp8_put8(q8, base + col, o, qmax);
-        }
+        if (Q) put8_bf16_q(y, base + col, o, q8, qsc, qmax);  // YDT == BF16 (launcher)
+        else Vec8<YDT>::store(y, base + col, o);
       }
     }
   }
@@ -66,12 +64,13 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const void* __restrict
 
 // Q (DADT == BF16 only): fused fp8 side output of the branch gradient da (common.h Fp8Out).
 template <int NCH, int DYDT, int DADT, bool Q = false>
-__global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const void* __restrict__ dy, const float* __restrict__ h,
+__global__ void __launch_bounds__(256, (NCH <= 2 ? 4 : 1)) rmsnorm_bwd_kernel(const void* __restrict__ dy, const float* __restrict__ h,
                                                           const float* __restrict__ w, const float* __restrict__ rstd,
                                                           const float* __restrict__ dres, float* __restrict__ dx,
                                                           void* __restrict__ da, float* __restrict__ part,
                                                           int64_t rows, int cols, Fp8Out q8) {
   float qmax = 0.f;
+  const float qsc = Q ? q8.scale[0] : 1.f;
   extern __shared__ __attribute__((aligned(16))) float sdw[];  // [4 waves][cols] weight-gradient partials
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -122,11 +121,8 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const void* __restrict
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] += rs * (g[c][j] - xh[c][j] * dot);
         Vec8<F32>::store(dx, base + col, o);
-        if (DADT >= 0) Vec8<(DADT >= 0 ? DADT : 0)>::store(da, base + col, o);
-        if (Q) {
-          round_bf16x8(o);
-          fp8_put8(q8, base + col, o, qmax);
-        }
+        if (Q) put8_bf16_q(da, base + col, o, q8, qsc, qmax);  // DADT == BF16 (launcher)
+        else if (DADT >= 0) Vec8<(DADT >= 0 ? DADT : 0)>::store(da, base + col, o);
       }
     }
   }

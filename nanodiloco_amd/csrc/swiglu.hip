@@ -17,6 +17,7 @@ __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const void* __restrict_
   const int f8 = F >> 3;
   const int64_t total = n * f8;
   float amax = 0.f;
+  const float qsc = Q ? q8.scale[0] : 1.f;
   for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < total; it += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = it / f8;
     const int c = (int)(it % f8) * 8;
@@ -25,11 +26,8 @@ __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const void* __restrict_
     Vec8<DT>::load(gu, r * 2 * F + F + c, u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = g[j] * sigm(g[j]) * u[j];
-    Vec8<DT>::store(out, r * F + c, o);
-    if (Q) {
-      round_bf16x8(o);
-      fp8_put8(q8, r * F + c, o, amax);
-    }
+    if (Q) put8_bf16_q(out, r * F + c, o, q8, qsc, amax);  // DT == BF16 (launcher)
+    else Vec8<DT>::store(out, r * F + c, o);
   }
   if (Q) block_amax_commit<256>(amax, q8.amax, q8.parts);
 }
@@ -40,6 +38,7 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const void* __restrict_
   const int f8 = F >> 3;
   const int64_t total = n * f8;
   float amax = 0.f;
+  const float qsc = Q ? q8.scale[0] : 1.f;
   for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < total; it += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = it / f8;
     const int c = (int)(it % f8) * 8;
@@ -53,13 +52,12 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const void* __restrict_
       du[j] = d[j] * g[j] * s;
       dg[j] = d[j] * u[j] * s * (1.f + g[j] * (1.f - s));
     }
-    Vec8<DT>::store(dgu, r * 2 * F + c, dg);
-    Vec8<DT>::store(dgu, r * 2 * F + F + c, du);
-    if (Q) {
-      round_bf16x8(dg);
-      round_bf16x8(du);
-      fp8_put8(q8, r * 2 * F + c, dg, amax);
-      fp8_put8(q8, r * 2 * F + F + c, du, amax);
+    if (Q) {  // DT == BF16 (launcher)
+      put8_bf16_q(dgu, r * 2 * F + c, dg, q8, qsc, amax);
+      put8_bf16_q(dgu, r * 2 * F + F + c, du, q8, qsc, amax);
+    } else {
+      Vec8<DT>::store(dgu, r * 2 * F + c, dg);
+      Vec8<DT>::store(dgu, r * 2 * F + F + c, du);
     }
   }
   if (Q) block_amax_commit<256>(amax, q8.amax, q8.parts);
