@@ -64,9 +64,10 @@ def parse():
     ap.add_argument("--tuned-gemm-file", default=None, help="alternative TunableOp table (A/B of tunings)")
     ap.add_argument("--hip-graph", action="store_true",
                     help="capture the micro-batch forward+backward in a HIP graph (launch-bound small models)")
-    ap.add_argument("--wgrad-overlap", type=int, default=0, choices=[0, 1, 2],
-                    help="issue weight-gradient GEMMs on a side HIP stream (overlaps the dgrad chain); off by "
-                         "default: beside hipBLASLt's stream-K GEMMs it stalls (docs/DESIGN.md)")
+    ap.add_argument("--wgrad-overlap", type=int, default=1, choices=[0, 1, 2],
+                    help="issue weight-gradient GEMMs on a side HIP stream (overlaps the dgrad chain), joined "
+                         "before every hipBLASLt GEMM (1, default: +0.4 %% per step, "
+                         "profiles/r4_wgrad_overlap_ab.md); 0 off; 2 unfenced (A/B only)")
     ap.add_argument("--wgrad-variant", default=None,
                     help="ND_WGRAD_VARIANT for the weight-gradient kernel (A/B of kernel schedules)")
     ap.add_argument("--attn-fused-stats", type=int, default=1, choices=[0, 1],

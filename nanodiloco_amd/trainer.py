@@ -75,8 +75,9 @@ class TrainArgs:
     hip_graph: str = "auto"        # capture the micro-batch fwd+bwd in a HIP graph (utils/graphs.py):
                                    # on | off | auto (= on for launch-bound models: GPU, < 100M params,
                                    # --inner-dp 1, no fp8, e.g. the reference's 10M default: 2.5x)
-    wgrad_overlap: bool = False    # weight-gradient GEMMs on a side HIP stream (ops/linear.py; GPU only;
-                                   # off: co-running with hipBLASLt stream-K GEMMs stalls, docs/DESIGN.md)
+    wgrad_overlap: bool = True     # weight-gradient GEMMs on a side HIP stream, joined before every library
+                                   # GEMM (ops/linear.py; GPU only): +0.4 % per step at round 4 HEAD
+                                   # (profiles/r4_wgrad_overlap_ab.md)
     checkpoint_dir: Optional[str] = None
     checkpoint_every: int = 0      # in outer steps (0 = only at the end when checkpoint_dir is set)
     stop_at_step: int = 0          # stop early (simulated preemption) after this inner step; 0 = run to total
