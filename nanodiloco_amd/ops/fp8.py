@@ -89,6 +89,8 @@ def mm8(a8: torch.Tensor, b8: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) 
         return gemm_pp_f8(a8, b8, sa, sb)
     if _GEMM["backend"] == "hip" and f8_nt_supported(a8, b8):
         return gemm_nt_f8(a8, b8, sa, sb)
+    from .linear import library_gemm_fence  # hipBLASLt stream-K must not co-run with side-stream wgrads
+    library_gemm_fence(a8.device if a8.is_cuda else None)
     return torch._scaled_mm(a8, b8.t(), sa, sb, out_dtype=torch.bfloat16)
 
 
@@ -308,19 +310,29 @@ class Fp8LinearFn(torch.autograd.Function):
 def _wgrad_bf16(gw, dy, x):
     if gw is None:
         return
-    if wgrad_supported(gw, dy, x):
-        wgrad(gw, dy, x)
-    else:
-        gw.add_(torch.mm(dy.t(), x).float())
+    from .linear import _wgrad  # side stream when the weight-gradient overlap is on
+    _wgrad(gw, dy, x)
 
 
 def _wgrad_f8(gw, dy8, x8, inv_dy, inv_x, dy=None):
     """gw += dy^T x from the fp8 operands (own kernel, csrc/gemm_wgrad.hip wgrad8_pp_kernel); shapes it does
-    not take fall back to the bf16 kernel on the dequantised operands (``dy``: the bf16 gradient if kept)."""
+    not take fall back to the bf16 kernel on the dequantised operands (``dy``: the bf16 gradient if kept).
+    With the weight-gradient overlap on (ops/linear.py ``set_wgrad_overlap``) it runs on the side stream like
+    the bf16 weight gradients: joined before every library GEMM and before the optimizer."""
     if gw is None:
         return
     if wgrad_f8_supported(gw, dy8, x8):
-        wgrad_f8(gw, dy8, x8, inv_dy, inv_x)
+        from . import linear as _lin
+        if _lin._OVERLAP["enabled"] and gw.is_cuda:
+            cur = torch.cuda.current_stream(gw.device)
+            side = _lin._side_stream(gw.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                wgrad_f8(gw, dy8, x8, inv_dy, inv_x)
+            _lin._OVERLAP["keep"].append((dy8, x8))
+            _lin._OVERLAP["pending"].add(side.device.index)
+        else:
+            wgrad_f8(gw, dy8, x8, inv_dy, inv_x)
     else:
         if dy is None:
             dy = (dy8.float() * inv_dy).to(torch.bfloat16)
