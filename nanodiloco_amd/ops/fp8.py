@@ -322,15 +322,15 @@ def _wgrad_f8(gw, dy8, x8, inv_dy, inv_x, dy=None):
     if gw is None:
         return
     if wgrad_f8_supported(gw, dy8, x8):
-        from . import linear as _lin
-        if _lin._OVERLAP["enabled"] and gw.is_cuda:
+        from .linear import _OVERLAP, _side_stream
+        if _OVERLAP["enabled"] and gw.is_cuda:
             cur = torch.cuda.current_stream(gw.device)
-            side = _lin._side_stream(gw.device)
+            side = _side_stream(gw.device)
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 wgrad_f8(gw, dy8, x8, inv_dy, inv_x)
-            _lin._OVERLAP["keep"].append((dy8, x8))
-            _lin._OVERLAP["pending"].add(side.device.index)
+            _OVERLAP["keep"].append((dy8, x8))
+            _OVERLAP["pending"].add(side.device.index)
         else:
             wgrad_f8(gw, dy8, x8, inv_dy, inv_x)
     else:
