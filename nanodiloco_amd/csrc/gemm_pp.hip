@@ -309,10 +309,8 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
           }
         const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
         const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
-        // ABL 8192 (A/B): gate / up (read again only in the backward) with the non-temporal policy
-        constexpr int GUP = (ABL & 8192) ? 2 : 0;
-        __builtin_amdgcn_raw_buffer_store_b128(pair16(g2[0], g2[1]), cr, og, 0, GUP);
-        __builtin_amdgcn_raw_buffer_store_b128(pair16(u2[0], u2[1]), cr, ou, 0, GUP);
+        __builtin_amdgcn_raw_buffer_store_b128(pair16(g2[0], g2[1]), cr, og, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(pair16(u2[0], u2[1]), cr, ou, 0, 0);
         if constexpr (Q != 0) {
           // e4m3 act (bitwise a separate cast of the bf16 act, which is not written): the lane's 8 units in
           // column order (pair16's permutation on the fp32 values), bf16-rounded, scaled, one 8-B store
@@ -775,8 +773,6 @@ template <int EPI, int HD = 64>
 int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
               const PPEpi& ep, hipStream_t s) {
   if (g_pp_variant == 1024) return launch_pp_v<EPI, HD, 1024>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
-  if constexpr (EPI == PP_SWIGLU)
-    if (g_pp_variant == 8192) return launch_pp_v<EPI, HD, 8192>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
   if constexpr (EPI == PP_STORE) {
     switch (g_pp_variant) {
       case 1: return launch_pp_v<EPI, HD, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
