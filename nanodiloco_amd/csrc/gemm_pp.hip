@@ -341,7 +341,6 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
       // (2 x PF x 4 VGPRs, taken from the next K-tile's fragment registers, free here) instead of one
       // -- one exposed HBM round trip per tile instead of per step
       constexpr int PF = Q != 0 ? 4 : DSW_PF;  // the fp8-output form needs the registers
-      constexpr int GUL = (ABL & 8192) ? 2 : 0;  // ABL 8192 (A/B): gate / up read once, non-temporal
       u32x4 gq[PF], uq[PF];
       auto gu_off = [&](int st, int half) -> uint32_t {
         const int a = st >> 1, bp = st & 1;
@@ -353,8 +352,8 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
       };
 #pragma unroll
       for (int st = 0; st < PF; ++st) {
-        gq[st] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st, 0), 0, GUL);
-        uq[st] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st, 1), 0, GUL);
+        gq[st] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st, 0), 0, 0);
+        uq[st] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st, 1), 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch above the first use (the scheduler sinks it)
 #pragma unroll
@@ -368,8 +367,8 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
           const int st = 2 * a + bp;
           const u32x4 gv = gq[st % PF], uv = uq[st % PF];
           if (st + PF < 16) {
-            gq[st % PF] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st + PF, 0), 0, GUL);
-            uq[st % PF] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st + PF, 1), 0, GUL);
+            gq[st % PF] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st + PF, 0), 0, 0);
+            uq[st % PF] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st + PF, 1), 0, 0);
           }
           __builtin_amdgcn_sched_barrier(0);
           // d(act) as fp32 in the same 8-unit order: swap the fp32 quads like pair16 does
@@ -774,8 +773,6 @@ template <int EPI, int HD = 64>
 int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
               const PPEpi& ep, hipStream_t s) {
   if (g_pp_variant == 1024) return launch_pp_v<EPI, HD, 1024>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
-  if constexpr (EPI == PP_DSWIGLU)
-    if (g_pp_variant == 8192) return launch_pp_v<EPI, HD, 8192>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
   if constexpr (EPI == PP_STORE) {
     switch (g_pp_variant) {
       case 1: return launch_pp_v<EPI, HD, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
