@@ -1059,7 +1059,10 @@ __global__ void __launch_bounds__(256) attn_neg_stats_kernel(const float* __rest
 // ABL (timing ablations, wrong results; ND_ATTN_DKDV_ABL): 1 no Q / dO / statistics DMA and no vmcnt wait,
 // 2 no barrier, 4 no softmax VALU (P = S, dS = dP), 8 no S / dP MFMAs, 16 no dV / dK MFMAs, 32 LDS fragments
 // read only in the first step
-template <int HD, bool ROPE_OUT, int BQ = 64, bool PAD = false, int NW = 4, int ABL = 0>
+template <int N> __device__ __forceinline__ void dkdv_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+
+// NB: Q / dO / statistics buffers in LDS; tile it + NB - 1 is in flight while tile it is computed
+template <int HD, bool ROPE_OUT, int BQ = 64, bool PAD = false, int NW = 4, int ABL = 0, int NB = 2>
 __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ NL, const float* __restrict__ ND, bf16_t* __restrict__ dK,
@@ -1070,10 +1073,10 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
   constexpr int RPI = 64 / CPR;            // rows per 1-KiB DMA wave-instruction
   constexpr int IPW = (BQ / RPI) / NW;     // DMA instructions per wave per operand tile
   constexpr int KB = 32 * NW;              // keys per workgroup
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[2 * BQ * HD];
-  __shared__ __attribute__((aligned(16))) bf16_t dOs[2 * BQ * HD];
-  __shared__ __attribute__((aligned(16))) float lse_s[2 * BQ];
-  __shared__ __attribute__((aligned(16))) float del_s[2 * BQ];
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[NB * BQ * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[NB * BQ * HD];
+  __shared__ __attribute__((aligned(16))) float lse_s[NB * BQ];
+  __shared__ __attribute__((aligned(16))) float del_s[NB * BQ];
 
   const int bk_count = B * nkv, rep = nh / nkv, nkb = (T + KB - 1) / KB;
   int kb, bk;  // see attn_bwd_dkdv_kernel
@@ -1123,7 +1126,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
   auto issue = [&](int it) {
     const int head = kvh * rep + it / ntq;
     const int q0 = qstart + (it % ntq) * BQ;
-    const int buf = it & 1;
+    const int buf = it % NB;
     const bf16_t* sq = Q + ((int64_t)b * T + q0) * ld + (int64_t)head * HD;
     const bf16_t* sd = dO + ((int64_t)b * T + q0) * ldo + (int64_t)head * HD;
 #pragma unroll
@@ -1138,15 +1141,29 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
       adma_b32(ND + rs, (uint32_t)(lane * 4), ds_a + (buf * BQ + wu * 64) * 4);
     }
   };
-  issue(0);
+#pragma unroll
+  for (int j = 0; j < NB - 1; ++j)
+    if (j < nit) issue(j);
   bf16x8 qa[NT], da[NT], tdo[2][NO], tq[2][NO];
   bool first = true;
   for (int it = 0; it < nit; ++it) {
-    if constexpr (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of tile it has landed
+    if constexpr (!(ABL & 1)) {  // this wave's part of tile it has landed; tiles it+1 .. it+NB-2 may stay in flight
+      if constexpr (NB > 2) {
+        constexpr int PT = 2 * IPW;  // per tile and wave, plus 2 statistics loads on waves < BQ / 64
+        if (it + NB - 2 < nit) {
+          if (wu < BQ / 64) dkdv_vm<(PT + 2) * (NB - 2)>();
+          else dkdv_vm<PT * (NB - 2)>();
+        } else {
+          dkdv_vm<0>();
+        }
+      } else {
+        dkdv_vm<0>();
+      }
+    }
     if constexpr (!(ABL & 2)) __syncthreads();        // everyone's; and tile it-1's buffer is free
-    if constexpr (!(ABL & 1)) if (it + 1 < nit) issue(it + 1);
+    if constexpr (!(ABL & 1)) if (it + NB - 1 < nit) issue(it + NB - 1);
     const int q0 = qstart + (it % ntq) * BQ;
-    const int buf = it & 1;
+    const int buf = it % NB;
     const bf16_t* Qt = Qs + buf * (BQ * HD);
     const bf16_t* dOt = dOs + buf * (BQ * HD);
     const float* lt = lse_s + buf * BQ;
@@ -1345,7 +1362,15 @@ static int bwd_fused_launch(const void* q, const void* k, const void* v, const v
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD, 8>), dim3((T + 255) / 256 * B * nkv), dim3(512),
                        0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
                        (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
-  else if (T % 128 == 0) {
+  else if (const char* nbe = getenv("ND_ATTN_DKDV_NB"); nbe && nbe[0] >= '2' && nbe[0] <= '4') {  // 64-query tiles, A/B
+#define ND_DN(X) hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 64, PAD, 4, 0, X>), dim3(nb * B * nkv), dim3(256), \
+      0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd, (bf16_t*)dk, (bf16_t*)dv, \
+      B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv))
+    if (nbe[0] == '2') ND_DN(2);
+    else if (nbe[0] == '3') ND_DN(3);
+    else ND_DN(4);
+#undef ND_DN
+  } else if (T % 128 == 0) {
     const char* ab = getenv("ND_ATTN_DKDV_ABL");  // timing ablations (wrong results)
     const int abl = ab ? atoi(ab) : 0;
     switch (abl) {
