@@ -619,3 +619,36 @@ def test_attention_bwd_dq_variants(B, T, nh, nkv, hd, pads, variant, monkeypatch
     nq, nk = nh * hd, nkv * hd
     for name, sl in (("dq", slice(0, nq)), ("dk", slice(nq, nq + nk)), ("dv", slice(nq + nk, None))):
         assert rel(g[:, sl], gr[:, sl]) < 3e-2, (name, rel(g[:, sl], gr[:, sl]))
+
+
+@pytest.mark.parametrize("B,T,nh,nkv,hd,pads", [
+    (2, 192, 4, 2, 64, None), (1, 1024, 4, 4, 64, None), (2, 320, 4, 4, 32, None), (1, 256, 2, 2, 128, None),
+    (2, 1024, 8, 2, 64, (0, 700)),
+])
+@pytest.mark.parametrize("nb", ["2", "3", "4"])
+def test_attention_dkdv_prefetch_depth_bitwise(B, T, nh, nkv, hd, pads, nb, monkeypatch):
+    """dK/dV with 64-query tiles and NB LDS buffers (ND_ATTN_DKDV_NB, profiles/r4_attention_dkdv_ablation.md):
+    the same 32-query steps in the same order as the default kernel, so dQ / dK / dV are bitwise equal."""
+    from nanodiloco_amd.ops.attention import key_start, rope_cache
+    ld = (nh + 2 * nkv) * hd
+    ks = None
+    if pads is not None:
+        mask = torch.ones(B, T, dtype=torch.long, device=DEV)
+        for b, p in enumerate(pads):
+            mask[b, :p] = 0
+        ks = key_start(mask)
+    qkv = torch.randn(B * T, ld, device=DEV).bfloat16()
+    cos, sin = rope_cache(T, hd, 10000.0, None, DEV)
+    do = torch.randn(B * T, nh * hd, device=DEV).bfloat16()
+
+    def grads():
+        x = qkv.clone().requires_grad_(True)
+        ops.attention(x, cos, sin, B, T, nh, nkv, hd, kstart=ks).backward(do)
+        return x.grad
+
+    monkeypatch.delenv("ND_ATTN_DKDV_NB", raising=False)
+    g0 = grads()
+    monkeypatch.setenv("ND_ATTN_DKDV_NB", nb)
+    g1 = grads()
+    assert torch.isfinite(g0.float()).all()
+    assert torch.equal(g0, g1)
