@@ -53,10 +53,11 @@ def parse():
     ap.add_argument("--inner-steps", type=int, default=100)
     ap.add_argument("--inner-dp", type=int, default=1)
     ap.add_argument("--ops", default="auto", choices=["auto", "hip", "torch"])
-    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
-                    help="collective backend (auto = nccl/RCCL on GPU); gloo lets several ranks share one GPU. "
-                         "An explicit backend at world size 1 still creates a one-rank process group and "
-                         "issues every collective (the RCCL path on one GPU)")
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo", "none"],
+                    help="collective backend (auto = nccl/RCCL on GPU, gloo on CPU); gloo lets several ranks share "
+                         "one GPU. At world size 1 every backend but 'none' still creates a one-rank process group "
+                         "and issues every collective, so the 1-GPU headline runs the same RCCL path (communicator "
+                         "init, bucketed all-reduce on the priority stream) as N=8; 'none' = no process group (A/B)")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--bucket-mb", type=float, default=128.0)
     ap.add_argument("--overlap-outer", action="store_true")
@@ -85,10 +86,10 @@ def parse():
     ap.add_argument("--fp8-wgrad", type=int, default=1, choices=[0, 1],
                     help="with --fp8: weight-gradient GEMMs in fp8 too (own kernel on the token-major fp8 "
                          "operands; default on)")
-    ap.add_argument("--fp8-gemm", default="pp", choices=["pp", "auto", "hip", "hipblaslt"],
+    ap.add_argument("--fp8-gemm", default="pp", choices=["pp", "auto", "hipblaslt"],
                     help="with --fp8: forward / input-gradient fp8 GEMMs: pp (default: the own fp8 ping-pong kernel "
                          "with the fused epilogues for every product), auto (hipBLASLt for the long-K N<=1024 plain "
-                         "products), hip (round-2 fp8 kernel) or hipblaslt")
+                         "products) or hipblaslt")
     ap.add_argument("--fp8-fused-epi", type=int, default=1, choices=[0, 1],
                     help="with --fp8 and --fp8-gemm pp: RoPE / SwiGLU fused into the fp8 GEMM epilogues")
     ap.add_argument("--fp8-keep-fused", default="none", choices=["none", "rope", "mlp", "both"],
@@ -121,11 +122,12 @@ def main():
     targs = TrainArgs(
         seed=1337, batch_size=a.batch_size, per_device_batch_size=a.micro_batch, seq_length=a.seq_len,
         warmup_steps=100, total_steps=H * max(1, -(-10_000 // H)), inner_steps=H, lr=4e-4, outer_lr=0.7,
-        llama_config_file=a.model, data="synthetic", ops=a.ops, backend=a.backend, inner_dp=a.inner_dp,
+        llama_config_file=a.model, data="synthetic", ops=a.ops, backend="auto" if a.backend == "none" else a.backend,
+        inner_dp=a.inner_dp,
         comm_dtype=a.comm_dtype, bucket_mb=a.bucket_mb, overlap_outer=a.overlap_outer, fp8=a.fp8,
         fp8_wgrad=bool(a.fp8_wgrad), fp8_keep_fused=a.fp8_keep_fused, tuned_gemm=not a.no_tuned_gemm and not a.tuned_gemm_file,
         hip_graph="on" if a.hip_graph else "off", wgrad_overlap=bool(a.wgrad_overlap), log_every=0, wandb="off",
-        phase_timing=False, force_collectives=a.backend != "auto" and world == 1)
+        phase_timing=False, force_collectives=a.backend != "none" and world == 1)
     tr = Trainer(targs)
     env, cfg, dl = tr.env, tr.llama_config, tr.diloco
     ops.set_wgrad_overlap(a.wgrad_overlap)  # mode 2 (unfenced A/B) is not a trainer option

@@ -930,17 +930,55 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
 }
 
 // ------------------------------------------------------------------------------------ launchers
-// grid order of the attention kernels (see attn_fwd_kernel); ND_ATTN_ORDER=0/1 for A/B
-static int attn_order() {
-  const char* e = getenv("ND_ATTN_ORDER");
-  return e ? atoi(e) : 1;
-}
-// dK/dV: grouping the key blocks of one (batch, kv head) is +3 % with GQA 32/4 in isolation and
-// +1.8 % inside the Llama-150M step (rocprof): off by default (ND_ATTN_DKDV_ORDER=1 for A/B)
-static int dkdv_order(int nh, int nkv) {
-  const char* e = getenv("ND_ATTN_DKDV_ORDER");
-  return e ? atoi(e) && nh == nkv : 0;
-}
+// Launch-time switches, read ONCE when the library loads (never per launch).  Only correct variants are
+// selectable in the product library; the wrong-result timing ablations (ABL bits other than the
+// forward's 32) are compiled only into a -DND_ABLATION build (`python -m nanodiloco_amd.csrc.build
+// --ablation` -> _lib/alt/libnd_kernels_ablation.so), so a stray ND_ATTN_*ABL variable cannot change
+// what a training job computes.
+struct AttnEnv {
+  int order = 1;        // ND_ATTN_ORDER: grid order (see attn_fwd_kernel)
+  int dkdv_order = 0;   // ND_ATTN_DKDV_ORDER: group the key blocks of one (batch, kv head); +1.8 % slower in-step
+  float thr = 8.f;      // ND_ATTN_THR: deferred-max threshold (log2 units; 0 = move the max on every increase)
+  bool fwd_reg = false; // ND_ATTN_FWD=r: register-staged forward
+  int fwd_var = 32;     // ND_ATTN_ABL: 32 (cheaper mask / v_max3 tree, 1.007-1.024x) or 0 (plain)
+  bool fwd_w8 = false, dq_w8 = false, dkdv_w8 = false;  // ND_ATTN_{FWD,DQ,DKDV}_W=8: 256-row blocks
+  int dkdv_nb = 0;      // ND_ATTN_DKDV_NB=2..4: 64-query dK/dV tiles with NB LDS buffers
+  bool dkdv_reg = false;   // ND_ATTN_DKDV=r: register-staged dK/dV (unfused backward)
+  bool dkdv_bq64 = false;  // ND_DKDV_BQ=64: 64-query tiles (unfused backward)
+  int fwd_abl = 0, dkdv_abl = 0;  // ND_ATTN_ABL / ND_ATTN_DKDV_ABL timing ablations: ND_ABLATION builds only
+};
+static const AttnEnv g_attn = [] {
+  AttnEnv c;
+  auto s = [](const char* k) { return getenv(k); };
+  if (const char* e = s("ND_ATTN_ORDER")) c.order = atoi(e);
+  if (const char* e = s("ND_ATTN_DKDV_ORDER")) c.dkdv_order = atoi(e);
+  if (const char* e = s("ND_ATTN_THR")) c.thr = (float)atof(e);
+  if (const char* e = s("ND_ATTN_FWD")) c.fwd_reg = e[0] == 'r';
+  if (const char* e = s("ND_ATTN_ABL")) {
+    const int v = atoi(e);
+    if (v == 0 || v == 32) c.fwd_var = v;
+#ifdef ND_ABLATION
+    else c.fwd_abl = v;
+#endif
+  }
+  if (const char* e = s("ND_ATTN_FWD_W")) c.fwd_w8 = e[0] == '8';
+  if (const char* e = s("ND_ATTN_DQ_W")) c.dq_w8 = e[0] == '8';
+  if (const char* e = s("ND_ATTN_DKDV_W")) c.dkdv_w8 = e[0] == '8';
+  if (const char* e = s("ND_ATTN_DKDV_NB"); e && e[0] >= '2' && e[0] <= '4') c.dkdv_nb = e[0] - '0';
+  if (const char* e = s("ND_ATTN_DKDV")) c.dkdv_reg = e[0] == 'r';
+  if (const char* e = s("ND_DKDV_BQ")) c.dkdv_bq64 = e[0] == '6';
+#ifdef ND_ABLATION
+  if (const char* e = s("ND_ATTN_DKDV_ABL")) c.dkdv_abl = atoi(e);
+#endif
+  return c;
+}();
+static int attn_order() { return g_attn.order; }
+static int dkdv_order(int nh, int nkv) { return g_attn.dkdv_order && nh == nkv; }
+
+// wrong-result ablation builds only (timing): ABL bits of attn_fwd_kernel / attn_bwd_dkdv_dma_kernel
+#ifdef ND_ABLATION
+ND_API int nd_attn_ablation_build() { return 1; }
+#endif
 
 template <int HD, bool PAD>
 static int fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, int B, int nh, int nkv, int T,
@@ -949,47 +987,45 @@ static int fwd_launch(const void* q, const void* k, const void* v, void* o, floa
   const int nqb = (T + 127) / 128;
   const dim3 g(nqb * B * nh), b(256);
   // deferred-max threshold (log2 units; ND_ATTN_THR for A/B, 0 = move the max on every increase)
-  const char* te = getenv("ND_ATTN_THR");
-  const float thr = te ? (float)atof(te) : 8.f;
-  // ND_ATTN_FWD: 'r' register-staged, else the LDS-DMA kernel (ND_ATTN_FWD_W=8: 256-query blocks,
-  // ND_ATTN_ABL: ablation / variant bits; profiles/r3_attention_experiments.md)
-  const char* fe = getenv("ND_ATTN_FWD");
-  const char fv = fe ? fe[0] : 'd';
+  const float thr = g_attn.thr;
   if (cosT)
     hipLaunchKernelGGL((attn_fwd_kernel<HD, true, false, PAD>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr, attn_order());
-  else if (T % 64 == 0 && fv != 'r') {
-    const char* ae = getenv("ND_ATTN_ABL");
-    const int abl = ae ? atoi(ae) : 32;  // default: the cheaper-mask / v_max3-tree variant (1.007-1.024x)
+  else if (T % 64 == 0 && !g_attn.fwd_reg) {
 #define ND_ABL(A)                                                                                                  \
   case A:                                                                                                          \
     hipLaunchKernelGGL((attn_fwd_kernel<HD, false, true, PAD, A>), g, b, 0, s, (const bf16_t*)q, (const bf16_t*)k, \
                        (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr,      \
                        attn_order());                                                                              \
     break;
-    const char* we = getenv("ND_ATTN_FWD_W");
-    bool w8 = false;
-    if constexpr (HD >= 64) w8 = we && we[0] == '8';  // HD 32: a 64-row tile is 4 DMA pieces, < 8 waves
-    if (w8) {
-      const dim3 g8((T + 255) / 256 * B * nh), b8(512);
-      switch (PAD ? 0 : abl) {
 #define ND_ABL8(A)                                                                                                   \
   case A:                                                                                                            \
     hipLaunchKernelGGL((attn_fwd_kernel<HD, false, true, PAD, A, 8>), g8, b8, 0, s, (const bf16_t*)q, (const bf16_t*)k, \
                        (const bf16_t*)v, (bf16_t*)o, lse, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, thr,        \
                        attn_order());                                                                                \
     break;
-        ND_ABL8(1) ND_ABL8(3) ND_ABL8(4) ND_ABL8(28) ND_ABL8(32)
+    const int abl = PAD ? 0 : (g_attn.fwd_abl ? g_attn.fwd_abl : g_attn.fwd_var);
+    bool w8 = false;
+    if constexpr (HD >= 64) w8 = g_attn.fwd_w8;  // HD 32: a 64-row tile is 4 DMA pieces, < 8 waves
+    if (w8) {
+      const dim3 g8((T + 255) / 256 * B * nh), b8(512);
+      switch (abl) {
+#ifdef ND_ABLATION
+        ND_ABL8(1) ND_ABL8(3) ND_ABL8(4) ND_ABL8(28)
+#endif
+        ND_ABL8(32)
         default: ND_ABL8(0)
-#undef ND_ABL8
       }
     } else {
-      switch (PAD ? 0 : abl) {
+      switch (abl) {
+#ifdef ND_ABLATION
         ND_ABL(1) ND_ABL(2) ND_ABL(3) ND_ABL(4) ND_ABL(7) ND_ABL(8) ND_ABL(12) ND_ABL(16) ND_ABL(20) ND_ABL(24) ND_ABL(28)
+#endif
         ND_ABL(32)
         default: ND_ABL(0)
       }
     }
+#undef ND_ABL8
 #undef ND_ABL
   }
   else
@@ -1260,15 +1296,13 @@ static void bwd_launch_t(const void* q, const void* k, const void* v, const void
                          int64_t ld, int64_t ldo, const float* cosT, const float* sinT, float scale, const int* ks,
                          hipStream_t s) {
   const int nb = (T + 127) / 128;
-  const char* ev = getenv("ND_ATTN_DKDV");
-  const bool dma = !ROPE && ws != nullptr && T % 64 == 0 && !(ev && ev[0] == 'r');
+  const bool dma = !ROPE && ws != nullptr && T % 64 == 0 && !g_attn.dkdv_reg;
   if (dma) {
     const int64_t n = (int64_t)B * nh * T;
     float *nl = ws, *nd = ws + n;
     hipLaunchKernelGGL(attn_neg_stats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lse, delta, nl, nd, n,
                        1.f / (scale * LOG2E));
-    const char* bq = getenv("ND_DKDV_BQ");  // "64": 64-query tiles (A/B); default 128 when T allows
-    if (!(bq && bq[0] == '6') && T % 128 == 0)
+    if (!g_attn.dkdv_bq64 && T % 128 == 0)  // 128-query tiles when T allows (ND_DKDV_BQ=64: 64, A/B)
       hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                          (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
                          (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
@@ -1342,8 +1376,7 @@ static int bwd_fused_launch(const void* q, const void* k, const void* v, const v
   float *nl = ws, *nd = ws + n;
   bool done = false;
   if constexpr (HD >= 64) {  // ND_ATTN_DQ_W=8: 256-query blocks
-    const char* we = getenv("ND_ATTN_DQ_W");
-    if (!done && we && we[0] == '8') {
+    if (!done && g_attn.dq_w8) {
       hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, ROPE_OUT, true, true, PAD, 8>), dim3((T + 255) / 256 * B * nh),
                          dim3(512), 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
                          lse, nullptr, (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd,
@@ -1355,30 +1388,29 @@ static int bwd_fused_launch(const void* q, const void* k, const void* v, const v
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, ROPE_OUT, true, true, PAD>), dim3(nb * B * nh), dim3(256), 0, s,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, nullptr,
                        (bf16_t*)dq, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, (const bf16_t*)o, nl, nd, ks, attn_order());
-  const char* kwe = getenv("ND_ATTN_DKDV_W");
   bool kw8 = false;
-  if constexpr (HD >= 64) kw8 = kwe && kwe[0] == '8' && T % 128 == 0;
+  if constexpr (HD >= 64) kw8 = g_attn.dkdv_w8 && T % 128 == 0;
   if (kw8)  // 256-key blocks
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD, 8>), dim3((T + 255) / 256 * B * nkv), dim3(512),
                        0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,
                        (bf16_t*)dk, (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv));
-  else if (const char* nbe = getenv("ND_ATTN_DKDV_NB"); nbe && nbe[0] >= '2' && nbe[0] <= '4') {  // 64-query tiles, A/B
+  else if (const int nbv = g_attn.dkdv_nb) {  // 64-query tiles, A/B
 #define ND_DN(X) hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 64, PAD, 4, 0, X>), dim3(nb * B * nkv), dim3(256), \
       0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd, (bf16_t*)dk, (bf16_t*)dv, \
       B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv))
-    if (nbe[0] == '2') ND_DN(2);
-    else if (nbe[0] == '3') ND_DN(3);
+    if (nbv == 2) ND_DN(2);
+    else if (nbv == 3) ND_DN(3);
     else ND_DN(4);
 #undef ND_DN
   } else if (T % 128 == 0) {
-    const char* ab = getenv("ND_ATTN_DKDV_ABL");  // timing ablations (wrong results)
-    const int abl = ab ? atoi(ab) : 0;
-    switch (abl) {
+    switch (g_attn.dkdv_abl) {  // always 0 outside an ND_ABLATION build
+#ifdef ND_ABLATION
 #define ND_DA(X) case X: hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD, 4, X>), dim3(nb * B * nkv), \
       dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd, (bf16_t*)dk, \
       (bf16_t*)dv, B, nh, nkv, T, ld, ldo, scale, cosT, sinT, ks, dkdv_order(nh, nkv)); break;
       ND_DA(1) ND_DA(2) ND_DA(3) ND_DA(4) ND_DA(8) ND_DA(16) ND_DA(24) ND_DA(32) ND_DA(28) ND_DA(63)
 #undef ND_DA
+#endif
       default:
         hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD>), dim3(nb * B * nkv), dim3(256), 0, s,
                            (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, nl, nd,

@@ -139,28 +139,51 @@ def _build_runtime(force, kern, todo) -> dict:
     return {"kernels": kern, "runtime": rt, "compiled": [os.path.basename(s) for s, _ in todo]}
 
 
-def build_revision(rev: str, jobs: int = 0, extra_flags=None, file_flags: bool = True, tag: str = "") -> str:
-    """Build libnd_kernels.so from the csrc/ of git revision `rev` into _lib/alt/ (for in-process
-    A/B against the working tree: device-to-device and run-to-run variance on MI355X is several
-    percent, so code versions are compared interleaved inside one process; see scripts/ab_kernels.py)."""
+def build_ablation(jobs: int = 0) -> str:
+    """The timing-ablation library: the working tree's csrc/ with -DND_ABLATION, which compiles in the
+    kernel variants that skip loads / barriers / MFMAs / stores (WRONG results, profiling only) into
+    _lib/alt/libnd_kernels_ablation.so.  The product library never contains them; load this one with
+    ND_KERNELS_LIB=<path> (ops/_ext.py) or ``_ext.load_library`` in the ablation scripts."""
+    return build_revision(None, jobs, ["-DND_ABLATION=1"], tag="ablation")
+
+
+def build_revision(rev, jobs: int = 0, extra_flags=None, file_flags: bool = True, tag: str = "") -> str:
+    """Build libnd_kernels.so from the csrc/ of git revision `rev` (None: the working tree) into _lib/alt/
+    (for in-process A/B against the working tree: device-to-device and run-to-run variance on MI355X is
+    several percent, so code versions are compared interleaved inside one process; see scripts/ab_kernels.py)."""
     import tempfile
     root = os.path.dirname(PKG)
-    sha = _run(["git", "-C", root, "rev-parse", "--short", rev]).stdout.strip()
-    out = os.path.join(LIB_DIR, "alt", f"libnd_kernels_{sha}{('_' + tag) if tag else ''}.so")
-    if os.path.exists(out):
-        return out
+    if rev is None:
+        srcs_wt = sorted(glob.glob(os.path.join(HERE, "*.hip")) + glob.glob(os.path.join(HERE, "*.h")))
+        out = os.path.join(LIB_DIR, "alt", f"libnd_kernels_{tag or 'wt'}.so")
+        key = _digest(srcs_wt, " ".join(extra_flags or []))
+        if os.path.exists(out) and not _stale(srcs_wt, out, " ".join(extra_flags or [])):
+            return out
+    else:
+        sha = _run(["git", "-C", root, "rev-parse", "--short", rev]).stdout.strip()
+        out = os.path.join(LIB_DIR, "alt", f"libnd_kernels_{sha}{('_' + tag) if tag else ''}.so")
+        if os.path.exists(out):
+            return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = _hipcc()
     with tempfile.TemporaryDirectory() as td:
-        names = _run(["git", "-C", root, "ls-tree", "--name-only", rev, "nanodiloco_amd/csrc/"]).stdout.split()
-        srcs = []
-        for n in names:
-            if n.endswith((".hip", ".h")):
+        if rev is None:
+            srcs = []
+            for n in srcs_wt:
                 dst = os.path.join(td, os.path.basename(n))
-                with open(dst, "w") as f:
-                    f.write(_run(["git", "-C", root, "show", f"{rev}:{n}"]).stdout)
+                shutil.copyfile(n, dst)
                 if n.endswith(".hip"):
                     srcs.append(dst)
+        else:
+            names = _run(["git", "-C", root, "ls-tree", "--name-only", rev, "nanodiloco_amd/csrc/"]).stdout.split()
+            srcs = []
+            for n in names:
+                if n.endswith((".hip", ".h")):
+                    dst = os.path.join(td, os.path.basename(n))
+                    with open(dst, "w") as f:
+                        f.write(_run(["git", "-C", root, "show", f"{rev}:{n}"]).stdout)
+                    if n.endswith(".hip"):
+                        srcs.append(dst)
         flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-I", td]
         flags += list(extra_flags or [])
 
@@ -175,6 +198,9 @@ def build_revision(rev: str, jobs: int = 0, extra_flags=None, file_flags: bool =
         # -Bsymbolic: the side library's references to its own kernel stubs must not bind to the
         # identically named symbols of the main library already loaded RTLD_GLOBAL
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,-Bsymbolic", "-o", out] + objs)
+    if rev is None:
+        with open(out + ".sha256", "w") as f:
+            f.write(key)
     return out
 
 
@@ -187,7 +213,12 @@ def main(argv=None):
     ap.add_argument("--extra-flags", default="", help="with --rev: extra hipcc flags (compiler-option A/B)")
     ap.add_argument("--no-file-flags", action="store_true", help="with --rev: drop the per-file flags")
     ap.add_argument("--tag", default="", help="with --rev: suffix of the side library's file name")
+    ap.add_argument("--ablation", action="store_true",
+                    help="build the timing-ablation library (-DND_ABLATION, wrong-result variants) into _lib/alt/")
     a = ap.parse_args(argv)
+    if a.ablation:
+        print(build_ablation(a.jobs))
+        return
     if a.rev:
         print(build_revision(a.rev, a.jobs, a.extra_flags.split(), not a.no_file_flags, a.tag))
         return

@@ -220,6 +220,12 @@ __global__ void __launch_bounds__(256) ce_generic_kernel(void* __restrict__ logi
   }
 }
 
+// ND_CE=r: the register kernel for bf16 rows too (A/B), read once at load
+static const bool g_ce_reg = [] {
+  const char* e = getenv("ND_CE");
+  return e && e[0] == 'r';
+}();
+
 ND_API int nd_ce_fwd_bwd(void* logits, int dt, const int64_t* targets, float* loss_sum, const float* scale,
                          int64_t n, int V, int ignore, float* lse_out, float* row_loss, float /*reserved*/,
                          hipStream_t s) {
@@ -230,8 +236,7 @@ ND_API int nd_ce_fwd_bwd(void* logits, int dt, const int64_t* targets, float* lo
       if (dt == BF16) hipLaunchKernelGGL((ce_reg_kernel<BF16, 4>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
       else hipLaunchKernelGGL((ce_reg_kernel<F32, 4>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
     } else {
-      const char* ev = getenv("ND_CE");
-      if (dt == BF16 && !(ev && ev[0] == 'r'))
+      if (dt == BF16 && !g_ce_reg)
         hipLaunchKernelGGL((ce_bf16_kernel<16>), g, b, 0, s, (bf16_t*)logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
       else if (dt == BF16) hipLaunchKernelGGL((ce_reg_kernel<BF16, 16>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
       else hipLaunchKernelGGL((ce_reg_kernel<F32, 16>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);

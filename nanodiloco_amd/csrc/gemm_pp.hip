@@ -746,11 +746,21 @@ int num_cus_pp() {
   return n;
 }
 
-// ablation / A-B builds: nd_gemm_pp_set_variant or ND_GEMM_PP_VARIANT (1024 = buffer-form pieces, correct;
-// the others are timing-only builds with wrong results)
+// A/B builds: nd_gemm_pp_set_variant or ND_GEMM_PP_VARIANT (read once at load).  The product library
+// accepts only the correct-result variants (0 default, 32 plain-policy stores, 256 direct stores, 288 both,
+// 1024 buffer-form pieces); the timing-only ablations with wrong results (1-16, 64, 128 and their sums)
+// exist only in a -DND_ABLATION build (csrc/build.py --ablation -> _lib/alt/).
+bool pp_variant_ok(int v) {
+#ifdef ND_ABLATION
+  return v >= 0;
+#else
+  return v == 0 || v == 32 || v == 256 || v == 288 || v == 1024;
+#endif
+}
 int g_pp_variant = [] {
   const char* e = getenv("ND_GEMM_PP_VARIANT");
-  return e ? atoi(e) : 0;
+  const int v = e ? atoi(e) : 0;
+  return pp_variant_ok(v) ? v : 0;
 }();
 
 
@@ -775,6 +785,7 @@ int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_
   if (g_pp_variant == 1024) return launch_pp_v<EPI, HD, 1024>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
   if constexpr (EPI == PP_STORE) {
     switch (g_pp_variant) {
+#ifdef ND_ABLATION
       case 1: return launch_pp_v<EPI, HD, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       case 2: return launch_pp_v<EPI, HD, 2>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       case 3: return launch_pp_v<EPI, HD, 3>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
@@ -782,9 +793,10 @@ int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_
       case 8: return launch_pp_v<EPI, HD, 8>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       case 15: return launch_pp_v<EPI, HD, 15>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       case 16: return launch_pp_v<EPI, HD, 16>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
-      case 32: return launch_pp_v<EPI, HD, 32>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       case 64: return launch_pp_v<EPI, HD, 64>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       case 128: return launch_pp_v<EPI, HD, 128>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+#endif
+      case 32: return launch_pp_v<EPI, HD, 32>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);    // plain-policy stores
       case 256: return launch_pp_v<EPI, HD, 256>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);  // direct stores
       case 288: return launch_pp_v<EPI, HD, 288>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);  // direct, plain policy
       default: break;
@@ -936,7 +948,9 @@ ND_API int nd_gemm_pp_dswiglu_f8q(const void* A, const void* B, const void* gu, 
                  : launch_pp_v<PP_DSWIGLU, 64, 0, 2, 1>(A, B, dgu8, M, F, K, lda, ldb, 2 * (int64_t)F, ep, s);
 }
 
+// returns the previous variant, or -1 (nothing changed) for a variant this build does not contain
 ND_API int nd_gemm_pp_set_variant(int v) {
+  if (!pp_variant_ok(v)) return -1;
   const int old = g_pp_variant;
   g_pp_variant = v;
   return old;

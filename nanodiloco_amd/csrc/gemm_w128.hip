@@ -395,7 +395,7 @@ int num_cus_w128() {
 
 int g_w128_nt = 1;   // non-temporal C stores
 int g_w128_ovl = 1;  // epilogue woven into each tile's last phase (0: between the tiles)
-int g_w128_abl = 0;  // ablation builds (profiling only, wrong results): nd_gemm_w128_set_ablation
+int g_w128_abl = 0;  // ablation variants (profiling only; -DND_ABLATION builds): nd_gemm_w128_set_ablation
 
 template <int EPI, int STP, bool OVL, int ABL = 0>
 int launch_w128_v(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
@@ -415,6 +415,7 @@ int launch_w128_v(const void* A, const void* B, void* C, int M, int N, int K, in
 template <int EPI>
 int launch_w128(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
                 hipStream_t s) {
+#ifdef ND_ABLATION
   if constexpr (EPI == W_STORE) {
     switch (g_w128_abl) {
       case 1: return launch_w128_v<EPI, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, s);
@@ -424,10 +425,11 @@ int launch_w128(const void* A, const void* B, void* C, int M, int N, int K, int6
       case 8: return launch_w128_v<EPI, 2, false, 8>(A, B, C, M, N, K, lda, ldb, ldc, s);
       case 16: return launch_w128_v<EPI, 2, false, 16>(A, B, C, M, N, K, lda, ldb, ldc, s);
       case 31: return launch_w128_v<EPI, 2, false, 31>(A, B, C, M, N, K, lda, ldb, ldc, s);
-      case 4096: return launch_w128_v<EPI, 2, true, 4096>(A, B, C, M, N, K, lda, ldb, ldc, s);
+      case 4096: return launch_w128_v<EPI, 2, true, 4096>(A, B, C, M, N, K, lda, ldb, ldc, s);  // exact multiples only
       default: break;
     }
   }
+#endif
   if (g_w128_ovl && K >= 2 * TK)
     return g_w128_nt ? launch_w128_v<EPI, 2, true>(A, B, C, M, N, K, lda, ldb, ldc, s)
                      : launch_w128_v<EPI, 0, true>(A, B, C, M, N, K, lda, ldb, ldc, s);
@@ -450,7 +452,11 @@ ND_API int nd_gemm_w128(const void* A, const void* B, void* C, int M, int N, int
   return launch_w128<W_STORE>(A, B, C, M, N, K, lda, ldb, ldc, s);
 }
 
+// the timing ablations (wrong results) exist only in a -DND_ABLATION build: elsewhere this returns -1
 ND_API int nd_gemm_w128_set_ablation(int v) {
+#ifndef ND_ABLATION
+  if (v != 0) return -1;
+#endif
   const int old = g_w128_abl;
   g_w128_abl = v;
   return old;

@@ -1048,6 +1048,19 @@ static int fit_kchunk(int K, int* S, int bk) {
   }
 }
 
+// ND_WGRAD_VARIANT (A/B runs), read once at load; outside -DND_ABLATION builds the wrong-result forms
+// ("nodma", "a<bits>") are dropped, i.e. the default kernel runs
+static const char* wgrad_env() {
+  static const char* v = [] {
+    const char* e = getenv("ND_WGRAD_VARIANT");
+#ifndef ND_ABLATION
+    if (e && (e[0] == 'n' || e[0] == 'a')) return (const char*)nullptr;
+#endif
+    return e;
+  }();
+  return v;
+}
+
 // Number of K splits for this shape (slab workspace = S * M * N floats when S > 1).
 ND_API int nd_wgrad_splits(int M, int N, int K) {
   int S;
@@ -1068,7 +1081,8 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
   // per-cluster and the static waves-4-7 form, measured +-0 e2e and were dropped.)  (Measured and dropped, see docs/DESIGN.md: a 4-deep
   // BK=32 ring with counted vmcnt, a 16x16x32-MFMA version and a quadrant-phase pipeline -- all
   // 3-15 % slower than this kernel on the Llama-150M shapes.)
-  const char* ev = getenv("ND_WGRAD_VARIANT");
+  // read once when the library loads (wgrad_env); wrong-result variants only in -DND_ABLATION builds
+  const char* ev = wgrad_env();
   const int variant = (ev && ev[0] == 'r') ? 1 : (ev && ev[0] == 'n') ? 4 : (ev && ev[0] == '4') ? 5 : 0;
   // the sched_group_barrier interleave (MFMA / 2 transposing reads) is opt-in ("dmas"): measured
   // 4-13 % SLOWER per kernel than the compiler's own schedule at 32k and 64k tokens, -1.7 % e2e
@@ -1085,6 +1099,7 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
                      hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<true>),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (attrp != hipSuccess) return (int)attrp;
+#ifdef ND_ABLATION
     if (ev && ev[0] == 'a') {  // timing ablations (wrong results)
       const int abl = atoi(ev + 1);
 #define ND_WA(X) case X: hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<true, X>), \
@@ -1095,6 +1110,7 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
 #undef ND_WA
       ND_LAUNCH_CHECK();
     }
+#endif
     // default: full half-tiles staged with FLAT-global LDS loads (bitwise the same as the buffer form,
     // 1.005x over the three Llama-150M shapes, profiles/r4_gdma_ab.md); "b": buffer loads only (A/B)
     if (!(ev && ev[0] == 'b'))
@@ -1112,7 +1128,8 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
     (void)attr4;
     hipLaunchKernelGGL(wgrad4_kernel, dim3(tiles * S), dim3(256), lds, s, (const bf16_t*)A, (const bf16_t*)B, C, slab,
                        M, N, K, lda, ldb, ldc, S, kchunk);
-  } else if (large && variant == 4) {  // "nodma": compute-only diagnostic
+#ifdef ND_ABLATION
+  } else if (large && variant == 4) {  // "nodma": compute-only diagnostic (wrong result)
     const int kchunk = fit_kchunk(K, &S, BK3);
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);
@@ -1121,7 +1138,8 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
     (void)attr_ok;
     hipLaunchKernelGGL((wgrad_dma_kernel<true, true>), dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A,
                        (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
-  } else if (large && variant != 1 && M >= 8 && N >= 8) {
+#endif
+  } else if (large && variant != 1 && variant != 4 && M >= 8 && N >= 8) {
     const int kchunk = fit_kchunk(K, &S, BK3);
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB

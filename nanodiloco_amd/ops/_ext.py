@@ -21,6 +21,10 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(os.path.dirname(_HERE), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libnd_kernels.so")
+# profiling-only override: ND_KERNELS_LIB=<path> loads another build as THE library, e.g. the timing-ablation
+# build (`python -m nanodiloco_amd.csrc.build --ablation` -> _lib/alt/libnd_kernels_ablation.so), whose
+# wrong-result kernel variants the product library does not contain
+LIB_PATH = os.environ.get("ND_KERNELS_LIB") or LIB_PATH
 
 _lib = None
 _lock = threading.Lock()
@@ -164,9 +168,6 @@ def _declare(L: ctypes.CDLL):
         "nd_fp8_cast": [P, I, L64, P, P, I, P, I, P],
         "nd_fp8_cast_t": [P, I, I, I, L64, P, P, P, I, P, I, P],
         # projection GEMMs (C = A B^T) and their fused epilogues
-        "nd_gemm_nt_f8": [P, P, P, I, I, I, L64, L64, L64, I, I, P, P, P],
-        "nd_gemm_set_group_m": [I],
-        "nd_gemm_set_f8_variant": [I],
         # ping-pong projection GEMMs (csrc/gemm_pp.hip)
         "nd_gemm_pp": [P, P, P, I, I, I, L64, L64, L64, P],
         "nd_gemm_pp_rope": [P, P, P, I, I, I, L64, L64, L64, P, P, I, I, I, P],

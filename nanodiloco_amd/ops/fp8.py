@@ -5,8 +5,8 @@ Recipe (per-tensor scaling, the common "delayed scaling" scheme):
   csrc/gemm_pp.hip F8: one ``v_mfma_scale_f32_16x16x128_f8f6f4`` per 128-deep K-tile of the same LDS image
   as the bf16 kernel; default ``set_fp8_gemm("pp")``), bf16 out.  The q|k|v projection keeps RoPE and the
   MLP keeps SwiGLU / its backward in that GEMM's epilogues (``Fp8RopeFn``, ``Fp8MLPFn``; on the dequantised
-  fp32 accumulator).  ``"hipblaslt"`` (``torch._scaled_mm``) and ``"hip"`` (the round-2 kernel,
-  csrc/gemm_f8.hip) are the A/B alternatives; they run the RoPE / SwiGLU passes separately;
+  fp32 accumulator).  ``"hipblaslt"`` (``torch._scaled_mm``) is the A/B alternative; it runs the RoPE /
+  SwiGLU passes separately;
 * dgrad    ``dx = dy @ W`` with dy in e5m2 (range for gradients), W^T in e4m3, same kernels;
 * wgrad    ``dW = dy^T x``: bf16 ``nd_wgrad`` by default; with ``wgrad_fp8`` the own fp8 kernel
   (``gemm.wgrad_f8``, csrc/gemm_wgrad.hip wgrad8_pp_kernel) straight from the token-major fp8 operands
@@ -33,7 +33,7 @@ from typing import Dict, Optional
 import torch
 
 from . import _ext
-from .gemm import (f8_nt_supported, gemm_nt_f8, gemm_pp_dswiglu_f8, gemm_pp_dswiglu_f8q, gemm_pp_f8, gemm_pp_rope_f8,
+from .gemm import (gemm_pp_dswiglu_f8, gemm_pp_dswiglu_f8q, gemm_pp_f8, gemm_pp_rope_f8,
                    gemm_pp_swiglu_f8, gemm_pp_swiglu_f8q, pp_f8_supported, wgrad, wgrad_f8, wgrad_f8_supported,
                    wgrad_supported)
 
@@ -45,8 +45,8 @@ TORCH_DT = {E4M3: torch.float8_e4m3fn, E5M2: torch.float8_e5m2}
 AMAX_PARTS = 64
 _FUSED = {"enabled": True}
 # "pp" (default): the ping-pong kernel on fp8 operands (csrc/gemm_pp.hip F8, 16x16x128 f8f6f4 MFMA), which
-# also carries the fused RoPE / SwiGLU epilogues; "hip": the round-2 one-wave-per-SIMD fp8 kernel
-# (csrc/gemm_f8.hip); "hipblaslt": torch._scaled_mm.  Shapes the own kernels do not take fall back to
+# also carries the fused RoPE / SwiGLU epilogues; "hipblaslt": torch._scaled_mm (A/B).  (The round-2
+# one-wave-per-SIMD fp8 kernel, 0.95x hipBLASLt, was removed in round 5.)  Shapes the own kernels do not take fall back to
 # torch._scaled_mm.
 _GEMM = {"backend": "pp"}
 # fp8 projections with their fused epilogues on the own fp8 GEMM: q|k|v + RoPE, gate|up + SwiGLU and the
@@ -57,8 +57,8 @@ _EPI = {"enabled": True}
 def set_fp8_gemm(backend: str) -> None:
     """fp8 forward / input-gradient GEMMs: "pp" (default: the own fp8 ping-pong kernel for every product),
     "auto" (hipBLASLt for the three long-K N <= 1024 plain products, where the own kernel runs 0.8x;
-    +0.2 % per step, within noise: profiles/r4_fp8_pp.md), "hip" (round-2 kernel) or "hipblaslt"."""
-    if backend not in ("auto", "pp", "hip", "hipblaslt"):
+    +0.2 % per step, within noise: profiles/r4_fp8_pp.md) or "hipblaslt"."""
+    if backend not in ("auto", "pp", "hipblaslt"):
         raise ValueError(backend)
     _GEMM["backend"] = backend
 
@@ -87,8 +87,6 @@ def mm8(a8: torch.Tensor, b8: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) 
     be = _GEMM["backend"]
     if (be == "pp" or (be == "auto" and _own_plain(a8, b8))) and pp_f8_supported(a8, b8):
         return gemm_pp_f8(a8, b8, sa, sb)
-    if _GEMM["backend"] == "hip" and f8_nt_supported(a8, b8):
-        return gemm_nt_f8(a8, b8, sa, sb)
     from .linear import library_gemm_fence  # hipBLASLt stream-K must not co-run with side-stream wgrads
     library_gemm_fence(a8.device if a8.is_cuda else None)
     return torch._scaled_mm(a8, b8.t(), sa, sb, out_dtype=torch.bfloat16)

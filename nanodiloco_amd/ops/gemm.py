@@ -1,13 +1,12 @@
-"""Own MFMA GEMMs (csrc/gemm_pp.hip, csrc/gemm_wgrad.hip, csrc/gemm_f8.hip).
+"""Own MFMA GEMMs (csrc/gemm_pp.hip, csrc/gemm_w128.hip, csrc/gemm_wgrad.hip).
 
 * ``gemm_pp``          C[M, N] = A[M, K] . B[N, K]^T on the ping-pong kernel (two waves per SIMD in
-                       opposite load / MFMA phases) -- the plain projection products when
-                       ``ops.linear.set_proj_gemm("pp")`` is selected (default: hipBLASLt, which it
-                       reaches 0.94-1.01x of, profiles/r3_gemm_pp.md).
+                       opposite load / MFMA phases) -- the plain projection / lm-head products when
+                       ``ops.linear.set_proj_gemm`` selects the own kernels (per-shape measurements:
+                       profiles/r4_gemm_w128.md, profiles/r5_gemm.md).
 * ``gemm_pp_rope``     the q|k|v projection with RoPE on q and k in the epilogue      } on the default
 * ``gemm_pp_swiglu``   the gate|up projection writing gu AND act = silu(gate) * up    } path (ops/linear.py
 * ``gemm_pp_dswiglu``  the down projection's dgrad fused with the SwiGLU backward     } LinearRopeFn, MLPFn)
-* ``gemm_nt_f8``       fp8 x fp8 -> bf16 (``--fp8 --fp8-gemm hip``)
 * ``wgrad``            ``gW[M, N] (fp32) += dY[K, M]^T @ X[K, N]`` -- the weight gradient of every projection
                        (default path): both operands staged through LDS as they lie in memory, fragments
                        by transposing LDS reads, ping-pong pairing, deterministic split-K.
@@ -37,40 +36,7 @@ def _aligned(t: torch.Tensor) -> bool:
     return t.data_ptr() % 16 == 0 and t.stride(-1) == 1 and t.stride(0) % 8 == 0
 
 
-def set_gemm_f8_variant(v: int) -> int:
-    """fp8 GEMM schedule (csrc/gemm_f8.hip g_f8_variant, A/B); returns the previous one."""
-    return _ext.lib().nd_gemm_set_f8_variant(int(v))
-
-
-def set_gemm_group_m(g: int) -> int:
-    """Tile grouping (m-panels per group) of the fp8 GEMM; 0/1 = row-major tiles."""
-    return int(_ext.lib().nd_gemm_set_group_m(int(g)))
-
-
 _F8_FMT = {torch.float8_e4m3fn: 0, torch.float8_e5m2: 1}
-
-
-def f8_nt_supported(a: torch.Tensor, b: torch.Tensor) -> bool:
-    """Shapes / layouts the own fp8 GEMM takes: K % 128, N % 8, row strides % 16, 16-B aligned."""
-    return (a.is_cuda and a.dim() == 2 and b.dim() == 2 and a.dtype in _F8_FMT and b.dtype in _F8_FMT
-            and a.shape[1] == b.shape[1] and a.shape[1] % 128 == 0 and b.shape[0] % 8 == 0
-            and a.stride(1) == 1 and b.stride(1) == 1 and a.stride(0) % 16 == 0 and b.stride(0) % 16 == 0
-            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
-
-
-def gemm_nt_f8(a: torch.Tensor, b: torch.Tensor, scale_a: torch.Tensor, scale_b: torch.Tensor,
-               out: torch.Tensor = None) -> torch.Tensor:
-    """out[M, N] (bf16) = scale_a * scale_b * a[M, K] . b[N, K]^T with a, b OCP fp8 (e4m3 / e5m2) and
-    the scales one-element fp32 device tensors -- the ``torch._scaled_mm(a, b.t(), scale_a, scale_b,
-    out_dtype=bf16)`` contract, on our MFMA kernel (``nd_gemm_nt_f8``)."""
-    M, K = a.shape
-    N = b.shape[0]
-    if out is None:
-        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
-    _ext.check(_ext.lib().nd_gemm_nt_f8(_ext.ptr(a), _ext.ptr(b), _ext.ptr(out), M, N, K, a.stride(0), b.stride(0),
-                                        out.stride(0), _F8_FMT[a.dtype], _F8_FMT[b.dtype], _ext.ptr(scale_a),
-                                        _ext.ptr(scale_b), _ext.stream_ptr(a.device)), "nd_gemm_nt_f8")
-    return out
 
 
 # ---- ping-pong kernels (csrc/gemm_pp.hip): two waves per SIMD in opposite LOAD / COMPUTE phases

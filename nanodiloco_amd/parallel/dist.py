@@ -111,12 +111,15 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
     # silent hang) after `timeout_s`; torchrun --max-restarts + --resume then restart from the last
     # outer-step checkpoint.
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-    pg_opts = _pg_options(backend, high_priority)
+    timeout = datetime.timedelta(seconds=timeout_s)
+    # one FRESH Options object per group: torch's _new_process_group_helper writes the group's timeout,
+    # split parent / colour, global ranks and name into the object it is given and the backend keeps a
+    # pointer to it, so a shared object would let every later new_group overwrite WORLD's settings
     if not dist.is_initialized():
-        kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+        kw = dict(backend=backend, timeout=timeout)
         if backend == "nccl":
             kw["device_id"] = dev  # eager RCCL communicator init
-            kw["pg_options"] = pg_opts
+            kw["pg_options"] = _pg_options(backend, high_priority)
         launched = "TORCHELASTIC_RUN_ID" in os.environ and "MASTER_PORT" in os.environ
         if world == 1 and not launched:
             # one rank outside torchrun: nothing to rendezvous with (a stray MASTER_ADDR without
@@ -132,13 +135,13 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
     else:
         for w in range(env.num_workers):  # every rank must create every group, in the same order
             ranks = list(range(w * inner_dp, (w + 1) * inner_dp))
-            g = dist.new_group(ranks, pg_options=pg_opts)
+            g = dist.new_group(ranks, timeout=timeout, pg_options=_pg_options(backend, high_priority))
             if w == env.worker:
                 env.inner_group = g
         if env.num_workers > 1:
             for r in range(inner_dp):
                 ranks = list(range(r, world, inner_dp))
-                g = dist.new_group(ranks, pg_options=pg_opts)
+                g = dist.new_group(ranks, timeout=timeout, pg_options=_pg_options(backend, high_priority))
                 if r == env.inner_rank:
                     env.outer_group = g
     return env

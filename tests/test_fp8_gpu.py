@@ -68,10 +68,10 @@ def test_fp8_weight_current_scaling(shape):
     assert wq.get(w, version=0) is wq and wq.version == 0
 
 
-@pytest.fixture(params=["auto", "pp", "hipblaslt", "hip"])
+@pytest.fixture(params=["auto", "pp", "hipblaslt"])
 def fp8_gemm(request):
     """The fp8 GEMM backends: the own ping-pong kernel (default; with the fused RoPE / SwiGLU epilogues
-    in the model), hipBLASLt, and the round-2 own kernel (csrc/gemm_f8.hip)."""
+    in the model), and hipBLASLt (A/B)."""
     old = fp8.fp8_gemm_backend()
     fp8.set_fp8_gemm(request.param)
     yield request.param
