@@ -58,6 +58,9 @@ def parse():
                          "one GPU. At world size 1 every backend but 'none' still creates a one-rank process group "
                          "and issues every collective, so the 1-GPU headline runs the same RCCL path (communicator "
                          "init, bucketed all-reduce on the priority stream) as N=8; 'none' = no process group (A/B)")
+    ap.add_argument("--comm-impl", default="auto", choices=["auto", "rccl", "c10d"],
+                    help="bulk collectives (initial broadcast, outer all-reduce buckets, inner-DDP spans): the own RCCL "
+                         "communicator (auto on GPU; parallel/rccl.py) or torch's process group (c10d, A/B)")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--bucket-mb", type=float, default=128.0)
     ap.add_argument("--overlap-outer", action="store_true")
@@ -123,7 +126,7 @@ def main():
         seed=1337, batch_size=a.batch_size, per_device_batch_size=a.micro_batch, seq_length=a.seq_len,
         warmup_steps=100, total_steps=H * max(1, -(-10_000 // H)), inner_steps=H, lr=4e-4, outer_lr=0.7,
         llama_config_file=a.model, data="synthetic", ops=a.ops, backend="auto" if a.backend == "none" else a.backend,
-        inner_dp=a.inner_dp,
+        inner_dp=a.inner_dp, comm_impl=a.comm_impl,
         comm_dtype=a.comm_dtype, bucket_mb=a.bucket_mb, overlap_outer=a.overlap_outer, fp8=a.fp8,
         fp8_wgrad=bool(a.fp8_wgrad), fp8_keep_fused=a.fp8_keep_fused, tuned_gemm=not a.no_tuned_gemm and not a.tuned_gemm_file,
         hip_graph="on" if a.hip_graph else "off", wgrad_overlap=bool(a.wgrad_overlap), log_every=0, wandb="off",
@@ -239,6 +242,8 @@ def main():
             "outer_step_wall_ms": round(1000.0 * dl.avg_sync_time, 3),
             "allreduce_calls_per_outer_step": dl.buckets_per_outer_step,
             "comm_backend": env.backend,
+            "comm_impl": env.comm_impl,
+            "rccl_calls": (dl.outer_comm.rccl.stats()["calls"] if dl.outer_comm.rccl is not None else None),
             "comm_dtype": a.comm_dtype,
             "model_tflops_per_gpu": round(mfu_flops / 1e12, 2),
             "final_loss": round(final_loss, 4),
@@ -254,7 +259,8 @@ def main():
         }
         print(json.dumps(out), flush=True)
     if env.is_distributed:
-        dist.destroy_process_group()
+        from nanodiloco_amd.parallel.dist import destroy_distributed
+        destroy_distributed()
 
 
 if __name__ == "__main__":

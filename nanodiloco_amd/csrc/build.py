@@ -2,6 +2,7 @@
 
   nanodiloco_amd/_lib/libnd_kernels.so   every csrc/*.hip, hipcc --offload-arch=gfx950 -O3
   nanodiloco_amd/_lib/libnd_runtime.so   csrc/runtime/*.cpp (host C++: token loader), g++ -O3
+  nanodiloco_amd/_lib/libnd_comm.so      csrc/comm/*.cpp (host C++: own RCCL communicator), hipcc -lrccl
 
 Usage:  python -m nanodiloco_amd.csrc.build [--force] [--jobs N] [--save-temps]
 Incremental: an object is rebuilt only when the content hash of its source / headers / flags changed.
@@ -136,7 +137,14 @@ def _build_runtime(force, kern, todo) -> dict:
         _run([cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", "-o", rt + ".tmp"] + rt_src)
         os.replace(rt + ".tmp", rt)
         _mark(rt_src, rt)
-    return {"kernels": kern, "runtime": rt, "compiled": [os.path.basename(s) for s, _ in todo]}
+    # own RCCL communicator (host code against librccl / the HIP runtime; no device code)
+    cm_src = sorted(glob.glob(os.path.join(HERE, "comm", "*.cpp")))
+    cm = os.path.join(LIB_DIR, "libnd_comm.so")
+    if cm_src and (force or _stale(cm_src, cm)):
+        _run([_hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", cm + ".tmp"] + cm_src + ["-lrccl"])
+        os.replace(cm + ".tmp", cm)
+        _mark(cm_src, cm)
+    return {"kernels": kern, "runtime": rt, "comm": cm, "compiled": [os.path.basename(s) for s, _ in todo]}
 
 
 def build_ablation(jobs: int = 0) -> str:

@@ -12,6 +12,10 @@ the host never blocks -- so a consumer kernel on bucket i overlaps the reduction
 
 SUM is used for every backend (gloo has no AVG); the 1/W factor is folded into the consumer
 kernel (outer Nesterov) or into the loss scale (inner DDP).
+
+Transport (``impl``): ``"rccl"`` -- the own RCCL communicator of the group (parallel/rccl.py,
+csrc/comm/nd_comm.cpp: its own high-priority stream, GPU-side event waits, watchdog), the default on
+GPU; ``"c10d"`` -- torch's process group (gloo on CPU; ``--comm-impl c10d`` on GPU for A/B).
 """
 from __future__ import annotations
 
@@ -45,6 +49,22 @@ class CommStats:
         self.__init__()
 
 
+class _RcclWork:
+    """c10d-Work-like handle of one own-RCCL collective: ``wait()`` = the current stream waits on the GPU."""
+
+    __slots__ = ("comm", "ticket")
+
+    def __init__(self, comm, ticket: int):
+        self.comm, self.ticket = comm, ticket
+
+    def wait(self):
+        self.comm.wait(self.ticket)
+        return True
+
+    def is_completed(self) -> bool:
+        return self.comm.query(self.ticket)
+
+
 class PendingAllReduce:
     def __init__(self, works, ranges, flat):
         self.works = works
@@ -70,14 +90,21 @@ class PendingAllReduce:
 class FlatCommunicator:
     """Bucketed async all-reduce / broadcast / all-gather on flat buffers for one process group."""
 
-    def __init__(self, group, group_size: int, bucket_mb: float = 128.0, enabled: bool = True, force: bool = False):
+    def __init__(self, group, group_size: int, bucket_mb: float = 128.0, enabled: bool = True, force: bool = False,
+                 impl: str = "c10d", device: Optional[torch.device] = None, timeout_s: float = 1800.0):
         """``force``: issue the collectives even for a one-member group (a one-rank process group from
-        ``init_distributed(force_pg=True)``), so the communicator path runs on a single GPU."""
+        ``init_distributed(force_pg=True)``), so the communicator path runs on a single GPU.
+        ``impl``: "rccl" (own communicator, GPU) or "c10d" (see module doc)."""
         self.group = group
         self.size = group_size
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.enabled = enabled and (group_size > 1 or force)
         self.stats = CommStats()
+        self.impl = impl if self.enabled else "none"
+        self.rccl = None
+        if self.enabled and impl == "rccl":
+            from .rccl import communicator_for
+            self.rccl = communicator_for(group, device, timeout_s)
 
     def all_reduce_async(self, flat: torch.Tensor, ranges: Optional[Sequence[Range]] = None) -> PendingAllReduce:
         if ranges is None:
@@ -85,7 +112,11 @@ class FlatCommunicator:
         works = []
         t0 = time.perf_counter()
         for a, b in ranges:
-            if self.enabled:
+            if self.rccl is not None:
+                works.append(_RcclWork(self.rccl, self.rccl.all_reduce(flat[a:b])))
+                self.stats.calls += 1
+                self.stats.bytes += (b - a) * flat.element_size()
+            elif self.enabled:
                 works.append(dist.all_reduce(flat[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
                 self.stats.calls += 1
                 self.stats.bytes += (b - a) * flat.element_size()
@@ -105,6 +136,12 @@ class FlatCommunicator:
     def broadcast(self, flat: torch.Tensor, src_group_rank: int = 0):
         if not self.enabled:
             return
+        if self.rccl is not None:
+            tickets = [self.rccl.broadcast(flat[a:b], src_group_rank)
+                       for a, b in plan_buckets(0, flat.numel(), flat.element_size(), self.bucket_bytes)]
+            for t in tickets:
+                self.rccl.wait(t)
+            return
         src = dist.get_global_rank(self.group, src_group_rank) if self.group not in (None, dist.group.WORLD) \
             else src_group_rank
         for a, b in plan_buckets(0, flat.numel(), flat.element_size(), self.bucket_bytes):
@@ -122,5 +159,8 @@ class FlatCommunicator:
             raise ValueError("all_gather_flat needs equal shards")
         lo = shard_ranges[0][0]
         out = flat[lo:lo + n * len(shard_ranges)]
+        if self.rccl is not None:  # in place: this member's shard already sits at its slot of `out`
+            self.rccl.wait(self.rccl.all_gather(out))
+            return
         mine = flat[a:b].clone()
         dist.all_gather_into_tensor(out, mine, group=self.group)

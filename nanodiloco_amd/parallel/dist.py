@@ -40,6 +40,8 @@ class DistEnv:
     worker: int = 0           # DiLoCo worker index  (rank // inner_dp)
     num_workers: int = 1      # world_size // inner_dp
     force_collectives: bool = False  # world size 1 with a live process group (force_pg)
+    comm_impl: str = "none"   # bulk-traffic transport: "rccl" (own communicator, parallel/rccl.py) | "c10d"
+    timeout_s: float = 1800.0
     inner_group: Optional[object] = None
     outer_group: Optional[object] = None
     world_group: Optional[object] = None
@@ -85,8 +87,24 @@ def comm_stream_high_priority(group=None) -> Optional[bool]:
         return None
 
 
+def _resolve_comm_impl(comm_impl: str, backend: str) -> str:
+    """auto: the own RCCL communicator whenever the backend is RCCL and libnd_comm.so is built; c10d
+    otherwise (gloo / CPU)."""
+    from . import rccl
+    if comm_impl == "auto":
+        return "rccl" if backend == "nccl" and rccl.available() else "c10d"
+    if comm_impl == "rccl" and backend != "nccl":
+        raise ValueError("--comm-impl rccl needs the nccl (RCCL) backend")
+    if comm_impl == "rccl" and not rccl.available():
+        raise RuntimeError(f"--comm-impl rccl but {rccl.LIB_PATH} is missing (python -m nanodiloco_amd.csrc.build)")
+    if comm_impl not in ("rccl", "c10d"):
+        raise ValueError(comm_impl)
+    return comm_impl
+
+
 def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[str] = None,
-                     timeout_s: float = 1800.0, force_pg: bool = False, high_priority: bool = True) -> DistEnv:
+                     timeout_s: float = 1800.0, force_pg: bool = False, high_priority: bool = True,
+                     comm_impl: str = "auto") -> DistEnv:
     rank = _env_int("RANK", 0)
     world = _env_int("WORLD_SIZE", 1)
     local_rank = _env_int("LOCAL_RANK", 0)
@@ -104,7 +122,7 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
         raise ValueError(f"world size {world} not divisible by inner_dp {inner_dp}")
     env = DistEnv(rank=rank, world_size=world, local_rank=local_rank, device=dev, backend="none",
                   inner_dp=inner_dp, inner_rank=rank % inner_dp, worker=rank // inner_dp,
-                  num_workers=world // inner_dp)
+                  num_workers=world // inner_dp, timeout_s=timeout_s)
     if world == 1 and not force_pg:
         return env
     # failure detection: a hung / failed collective surfaces as an error on every rank (instead of a
@@ -127,6 +145,7 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
             kw.update(store=dist.HashStore(), rank=0, world_size=1)
         dist.init_process_group(**kw)
     env.backend = backend
+    env.comm_impl = _resolve_comm_impl(comm_impl, backend)
     env.force_collectives = world == 1
     env.world_group = dist.group.WORLD
     if inner_dp == 1:
@@ -148,6 +167,8 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
 
 
 def destroy_distributed():
+    from .rccl import destroy_communicators
+    destroy_communicators()
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -53,6 +53,8 @@ class TrainArgs:
     data: str = "auto"             # auto | synthetic | memmap | hf
     ops: str = "auto"              # auto | hip | torch
     backend: str = "auto"          # auto | nccl | gloo
+    comm_impl: str = "auto"        # auto | rccl | c10d: bulk collectives on the own RCCL communicator
+                                   # (parallel/rccl.py; auto = whenever the backend is nccl) or torch's group
     device: str = "auto"           # auto | cpu | cuda
     inner_dp: int = 1
     outer_momentum: float = 0.9
@@ -155,7 +157,8 @@ class Trainer:
         ops.set_wgrad_overlap(a.wgrad_overlap)
         ops.set_deterministic(a.deterministic)
         self.env = env or init_distributed(a.backend, a.inner_dp, device=None if a.device == "auto" else a.device,
-                                           timeout_s=a.collective_timeout_s, force_pg=a.force_collectives)
+                                           timeout_s=a.collective_timeout_s, force_pg=a.force_collectives,
+                                           comm_impl=a.comm_impl)
         e = self.env
         if e.device.type == "cuda" and a.tuned_gemm:
             from .ops.tuned_gemm import enable_tuned_gemms

@@ -123,6 +123,42 @@ def main():
     sync()
     check(torch.equal(b, b0), "bucketed broadcast + sub-group all-gather")
 
+    # ---- the own RCCL communicator (parallel/rccl.py, csrc/comm/nd_comm.cpp): bucketed in-place all-reduce
+    # with GPU-side waits, broadcast, in-place all-gather, its high-priority stream, the c10d result
+    if not CPU:
+        from nanodiloco_amd.parallel import rccl
+        check(env.comm_impl == "rccl", f"own RCCL communicator selected by default (got {env.comm_impl})")
+        oc = FlatCommunicator(None, 1, bucket_mb=1.0, force=True, impl="rccl", device=dev, timeout_s=120.0)
+        check(oc.rccl is not None and oc.rccl.size == 1, "own communicator initialised (ncclCommInitRank via the store)")
+        x2 = ref.clone()
+        p2 = oc.all_reduce_async(x2)
+        for i in range(len(p2)):
+            p2.wait(i)
+        y2 = x2 * 2
+        sync()
+        check(len(p2) == nb and torch.equal(x2, ref) and torch.equal(y2, ref * 2), "own RCCL bucketed all-reduce exact")
+        st = oc.rccl.stats()
+        lo, hi = torch.cuda.Stream.priority_range()
+        check(st["calls"] >= nb and st["priority"] == hi, f"own RCCL stream at the highest priority ({st})")
+        b2 = torch.arange(40_000, device=dev, dtype=torch.float32)
+        oc.broadcast(b2, 0)
+        oc.all_gather_flat(b2, [(0, 40_000)], 0)
+        sync()
+        check(torch.equal(b2, b0) and all(p2.works[i].is_completed() for i in range(len(p2))),
+              "own RCCL broadcast + in-place all-gather")
+        # the consumer really waits for the collective: a long all-reduce followed at once by a consumer kernel
+        big = torch.ones(64 << 20, device=dev)
+        t = oc.rccl.all_reduce(big)
+        oc.rccl.wait(t)
+        s2 = big.sum()
+        check(float(s2.item()) == float(64 << 20) and oc.rccl.error() == 0, "consumer ordered after the collective")
+        check(rccl.version() is not None and rccl.version() > 0, f"RCCL version {rccl.version()}")
+        cc = DistEnv(device=dev, backend="nccl", force_collectives=True, comm_impl="c10d")
+        m_r, s_r, _, dlr = train_run(env, False)
+        m_c, s_c, _, dlc = train_run(cc, False)
+        check(dlr.outer_comm.impl == "rccl" and dlc.outer_comm.impl == "c10d", "Diloco on own RCCL vs c10d")
+        check(torch.equal(m_r, m_c) and torch.equal(s_r, s_c), "own RCCL == c10d ProcessGroupNCCL, bitwise")
+
     # ---- Diloco outer steps (pipelined and overlapped) + inner-DDP hooks from the autograd thread
     off = DistEnv(device=dev)  # collectives off: the oracle
     gl = DistEnv(device=dev, backend="gloo", force_collectives=True, inner_group=gloo, outer_group=gloo,
@@ -132,7 +168,7 @@ def main():
         m_off, s_off, _, _ = train_run(off, overlap)
         m_gl, s_gl, _, _ = train_run(gl, overlap) if gpu_gloo else (m_off, s_off, None, None)
         check(dl.outer_comm.enabled and dl.outer_comm.stats.calls > 0 and dl.inner_comm.stats.calls > 0,
-              f"overlap={overlap}: outer and inner collectives issued on RCCL")
+              f"overlap={overlap}: outer and inner collectives issued on RCCL ({dl.outer_comm.impl})")
         check(all(h == CFG["num_hidden_layers"] for h in hooks), f"overlap={overlap}: every layer hook fired")
         check(torch.equal(m_nc, m_off) and torch.equal(s_nc, s_off), f"overlap={overlap}: RCCL == no-comm, bitwise")
         check(torch.equal(m_nc, m_gl) and torch.equal(s_nc, s_gl), f"overlap={overlap}: RCCL == gloo, bitwise")
@@ -147,7 +183,8 @@ def main():
     ph = dl.outer_phase_ms()
     check(CPU and ph == {} or set(ph) == {"pseudograd_ms", "allreduce_ms", "outer_update_ms"} and all(v >= 0 for v in ph.values()),
           f"outer phase spans {ph}")
-    dist.destroy_process_group()
+    from nanodiloco_amd.parallel.dist import destroy_distributed
+    destroy_distributed()
     print("RCCL_CHECK_PASSED", flush=True)
 
 
