@@ -27,6 +27,10 @@ typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{a, b}), bf16x2_t));
 }
+// logistic sigmoid with the hardware reciprocal (v_rcp_f32, 1 ulp) and exponential: 4 VALU.  A plain
+// `1.f / (1.f + e)` compiles to the IEEE division sequence (div_scale / rcp / 4 fma / div_fmas / div_fixup,
+// 11 VALU), which made up half of the fused SwiGLU-backward GEMM epilogue.  x -> -inf: rcp(inf) = 0.
+__device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float lo_bf(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float hi_bf(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 

@@ -187,7 +187,7 @@ __device__ __forceinline__ u32x4 pair16(const f32x4& x, const f32x4& y) {
   return d;
 }
 __device__ __forceinline__ float rbf(float x) { return lo_bf(pack2(x, 0.f)); }
-__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+__device__ __forceinline__ float silu(float g) { return g * fast_sigmoid(g); }
 
 // ---- epilogue of one tile: the wave's 128 x 64 accumulator block (rows 128 g + .., columns 64 wn + ..)
 // of the tile at (m0, n0) -> the fused output(s).  Exactly NStores<EPI> 16-B buffer stores per wave
@@ -393,7 +393,7 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
             const float d = e < 4 ? d0[e] : d1[e - 4];
             const float gg = (e & 1) ? hi_bf(gw[e >> 1]) : lo_bf(gw[e >> 1]);
             const float uu = (e & 1) ? hi_bf(uw[e >> 1]) : lo_bf(uw[e >> 1]);
-            const float sg = 1.f / (1.f + __expf(-gg));
+            const float sg = fast_sigmoid(gg);
             du[e] = d * gg * sg;
             dg[e] = d * uu * sg * (1.f + gg * (1.f - sg));
           }

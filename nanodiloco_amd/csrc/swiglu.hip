@@ -9,7 +9,7 @@
 
 using namespace nd;
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float sigm(float x) { return fast_sigmoid(x); }
 
 template <int DT, bool Q = false>
 __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const void* __restrict__ gu, void* __restrict__ out,

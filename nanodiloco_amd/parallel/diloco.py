@@ -69,10 +69,10 @@ class Diloco:
         self.debug_checks = debug_checks
         e = self.env
         f = e.force_collectives
-        kw = dict(force=f, impl=e.comm_impl, device=e.device, timeout_s=e.timeout_s)
-        self.outer_comm = FlatCommunicator(e.outer_group, e.num_workers, bucket_mb, **kw)
-        self.inner_comm = FlatCommunicator(e.inner_group, e.inner_dp, bucket_mb, **kw)
-        self.world_comm = FlatCommunicator(e.world_group, e.world_size, bucket_mb, **kw)
+        kw = dict(impl=e.comm_impl, device=e.device, timeout_s=e.timeout_s)
+        self.outer_comm = FlatCommunicator(e.outer_group, e.num_workers, bucket_mb, force=f, **kw)
+        self.inner_comm = FlatCommunicator(e.inner_group, e.inner_dp, bucket_mb, force=f and e.force_inner_ddp, **kw)
+        self.world_comm = FlatCommunicator(e.world_group, e.world_size, bucket_mb, force=f, **kw)
         n = self.store.numel
         # shard of the flat vector this GPU reduces over the outer group (two-level mode)
         k = e.inner_dp

@@ -40,6 +40,10 @@ class DistEnv:
     worker: int = 0           # DiLoCo worker index  (rank // inner_dp)
     num_workers: int = 1      # world_size // inner_dp
     force_collectives: bool = False  # world size 1 with a live process group (force_pg)
+    # with force_collectives: also run the inner-DDP gradient all-reduce of a ONE-GPU worker (a no-op in the
+    # math, 12+ collectives per inner step: tests only -- the bench / trainer keep it off, so a one-rank
+    # headline step costs what a DiLoCo worker of the N=8 run costs)
+    force_inner_ddp: bool = False
     comm_impl: str = "none"   # bulk-traffic transport: "rccl" (own communicator, parallel/rccl.py) | "c10d"
     timeout_s: float = 1800.0
     inner_group: Optional[object] = None
@@ -65,7 +69,7 @@ def _pg_options(backend: str, high_priority: bool):
     bucketed outer all-reduce that ``--overlap-outer`` issues beside the next round's first inner step
     (and the inner-DDP gradient buckets beside the backward) is then scheduled ahead of the compute
     queue's kernels when both are ready."""
-    if backend != "nccl" or not high_priority:
+    if backend != "nccl" or not high_priority or os.environ.get("ND_COMM_PRIORITY", "high") == "normal":
         return None
     try:
         from torch.distributed import ProcessGroupNCCL

@@ -129,6 +129,8 @@ class RcclCommunicator:
         self._h = ctypes.c_void_p()
         idbuf = ctypes.create_string_buffer(uid, nbytes)
         dev_index = device.index if device.type == "cuda" and device.index is not None else 0
+        if os.environ.get("ND_COMM_PRIORITY", "high") == "normal":  # A/B of the stream priority
+            high_priority = False
         _check(L.nd_comm_init(ctypes.byref(self._h), self.size, idbuf, self.rank, dev_index, int(high_priority),
                               float(timeout_s)), f"ncclCommInitRank({key})")
         self.key = key

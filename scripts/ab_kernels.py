@@ -93,7 +93,7 @@ def workloads(what):
         out["attn_bwd"] = bwd
     elif what == "epi":  # the fused-epilogue ping-pong GEMMs at the Llama-150M bench shapes
         from nanodiloco_amd.ops import gemm as G
-        M, d, F = 65536, 1024, 2688
+        M, d, F = 131072, 1024, 2688
         x = (torch.randn(M, d, device="cuda") * 0.5).bfloat16()
         wq = (torch.randn(3 * d, d, device="cuda") * 0.05).bfloat16()
         wgu = (torch.randn(2 * F, d, device="cuda") * 0.05).bfloat16()
@@ -103,6 +103,10 @@ def workloads(what):
         out["rope"] = lambda: G.gemm_pp_rope(x, wq, cos, sin, 1024, 64, 2 * d)
         out["swiglu"] = lambda: G.gemm_pp_swiglu(x, wgu)
         out["dswiglu"] = lambda: G.gemm_pp_dswiglu(x, wdt, gu)
+        # the plain products of the same shapes: what each fused epilogue costs on top
+        out["qkv_plain"] = lambda: G.gemm_pp(x, wq)
+        out["gu_plain"] = lambda: G.gemm_pp(x, wgu)
+        out["down_dgrad_plain"] = lambda: G.gemm_pp(x, wdt)
     elif what == "wgrad":
         from nanodiloco_amd.ops.gemm import wgrad
         for name, (M, N) in {"qkv": (3072, 1024), "o": (1024, 1024), "gate_up": (5376, 1024),

@@ -85,6 +85,7 @@ def main():
     from nanodiloco_amd import ops
     ops.set_deterministic(True)  # no float atomics: two runs of the same step are bitwise equal
     env = init_distributed(BACKEND, device="cpu" if CPU else None, force_pg=True)
+    env.force_inner_ddp = True  # exercise the inner-DDP hooks on RCCL too (off in the trainer / bench)
     dev = env.device
     check(dist.is_initialized() and dist.get_backend() == BACKEND and env.backend == BACKEND,
           f"one-rank {BACKEND} group")
@@ -153,7 +154,7 @@ def main():
         s2 = big.sum()
         check(float(s2.item()) == float(64 << 20) and oc.rccl.error() == 0, "consumer ordered after the collective")
         check(rccl.version() is not None and rccl.version() > 0, f"RCCL version {rccl.version()}")
-        cc = DistEnv(device=dev, backend="nccl", force_collectives=True, comm_impl="c10d")
+        cc = DistEnv(device=dev, backend="nccl", force_collectives=True, comm_impl="c10d", force_inner_ddp=True)
         m_r, s_r, _, dlr = train_run(env, False)
         m_c, s_c, _, dlc = train_run(cc, False)
         check(dlr.outer_comm.impl == "rccl" and dlc.outer_comm.impl == "c10d", "Diloco on own RCCL vs c10d")
@@ -161,7 +162,8 @@ def main():
 
     # ---- Diloco outer steps (pipelined and overlapped) + inner-DDP hooks from the autograd thread
     off = DistEnv(device=dev)  # collectives off: the oracle
-    gl = DistEnv(device=dev, backend="gloo", force_collectives=True, inner_group=gloo, outer_group=gloo,
+    gl = DistEnv(device=dev, backend="gloo", force_collectives=True, force_inner_ddp=True, inner_group=gloo,
+                 outer_group=gloo,
                  world_group=gloo)
     for overlap in (False, True):
         m_nc, s_nc, hooks, dl = train_run(env, overlap)
