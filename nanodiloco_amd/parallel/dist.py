@@ -106,6 +106,20 @@ def _resolve_comm_impl(comm_impl: str, backend: str) -> str:
     return comm_impl
 
 
+def claim_compute_queues(dev: torch.device) -> None:
+    """Give the compute stream and the weight-gradient side stream their HIP hardware queues BEFORE any
+    communicator exists.  HIP maps streams onto its hardware queues (GPU_MAX_HW_QUEUES, 4 here) in creation
+    / first-use order; when RCCL's and c10d's streams are created first, the two compute streams land on
+    other queues and the overlapped backward ran 2 % slower (bench.py, one-rank group vs none, with the
+    side stream on: 330.6 vs 323.6 ms per step; serialized: equal -- round 5, gpurun_out r5d / r5g)."""
+    torch.zeros(1, device=dev).add_(1)  # first use of the compute (null) stream
+    from ..ops.linear import _side_stream
+    side = _side_stream(dev)
+    with torch.cuda.stream(side):
+        torch.zeros(1, device=dev).add_(1)
+    torch.cuda.synchronize(dev)
+
+
 def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[str] = None,
                      timeout_s: float = 1800.0, force_pg: bool = False, high_priority: bool = True,
                      comm_impl: str = "auto") -> DistEnv:
@@ -120,6 +134,7 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
     if use_cuda:
         torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
         dev = torch.device("cuda", torch.cuda.current_device())
+        claim_compute_queues(dev)
     else:
         dev = torch.device("cpu")
     if world % inner_dp:
