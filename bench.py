@@ -97,6 +97,8 @@ def parse():
                     help="with --fp8 and --fp8-gemm pp: RoPE / SwiGLU fused into the fp8 GEMM epilogues")
     ap.add_argument("--fp8-keep-fused", default="none", choices=["none", "rope", "mlp", "both"],
                     help="with --fp8: projections that stay on the bf16 fused-epilogue GEMMs")
+    ap.add_argument("--fp8-lm-head", type=int, default=1, choices=[0, 1],
+                    help="with --fp8: the lm head's three GEMMs in fp8 on the own kernels (1, default) or bf16 (0)")
     ap.add_argument("--fp8-fused-quant", type=int, default=1, choices=[0, 1],
                     help="with --fp8: operand quantisation fused into the producing kernels (0: separate casts)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
@@ -116,6 +118,7 @@ def main():
         _fp8.set_fp8_gemm(a.fp8_gemm)
         _fp8.set_fp8_fused_epilogues(bool(a.fp8_fused_epi))
         _fp8.set_fp8_keep_fused(a.fp8_keep_fused)
+        _fp8.set_fp8_lm_head(bool(a.fp8_lm_head))
     if a.wgrad_variant:
         os.environ["ND_WGRAD_VARIANT"] = a.wgrad_variant
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -254,6 +257,7 @@ def main():
             "fp8_gemm": a.fp8_gemm if a.fp8 else None,
             "fp8_fused_epilogues": bool(a.fp8_fused_epi) if a.fp8 else None,
             "fp8_keep_fused": a.fp8_keep_fused if a.fp8 else None,
+            "fp8_lm_head": bool(a.fp8_lm_head) if a.fp8 else None,
             "dgrad_transposed": ops.dgrad_transposed_enabled(),
             "ops": ops.get_backend() if a.ops != "auto" else ("hip" if env.device.type == "cuda" else "torch"),
         }

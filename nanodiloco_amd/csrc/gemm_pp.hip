@@ -237,8 +237,8 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
         }
         if constexpr (EPI == PP_ROPE) {
           // the wave's 64 columns are one 64-wide head (or two 32-wide ones): column block b pairs
-          // with b + HD / 32 in the same lane; v columns (>= rope_cols) pass through
-          const bool rot = n0 + wn * 64 < ep.rope_cols;
+          // with b + HD / 32 in the same lane.  Only q / k waves get here (pp_epilogue_any: v waves run
+          // the plain store epilogue), so no per-element selects
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
             if (((b * 16) % HD) >= HALFD) continue;
@@ -247,10 +247,9 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
             const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float c1 = rot ? cc[r] : 1.f, s1 = rot ? ss[r] : 0.f;
               const float x1 = v[b][r], x2 = v[p][r];
-              v[b][r] = x1 * c1 - x2 * s1;
-              v[p][r] = x2 * c1 + x1 * s1;
+              v[b][r] = x1 * cc[r] - x2 * ss[r];
+              v[p][r] = x2 * cc[r] + x1 * ss[r];
             }
           }
         }
@@ -451,6 +450,24 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
       }
     }
   }
+
+// the q|k|v epilogue per wave: its 64 columns are all q / k (RoPE) or all v (rope_cols % 64 == 0), so a
+// wave-uniform branch picks the RoPE body or the plain store body -- the v waves load no tables, whose
+// vmcnt waits would also drain the LDS-DMA pieces issued just before them (both bodies store NStores = 16)
+template <int EPI, int HD, int ABL, int F8 = 0, int Q = 0>
+__device__ __forceinline__ void pp_epilogue_any(const f32x4 (&acc)[8][4], bf16_t* __restrict__ C, int M, int N,
+                                                int64_t ldc, const PPEpi& ep, int m0, int n0, int g, int wn, int w,
+                                                int lane, char* smem, float sc, float qs, float& qmax) {
+  if constexpr (EPI == PP_ROPE) {
+    static_assert(NStores<PP_ROPE>::v == NStores<PP_STORE>::v, "counted waits assume equal store counts");
+    if (n0 + wn * 64 < ep.rope_cols)
+      pp_epilogue<PP_ROPE, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
+    else
+      pp_epilogue<PP_STORE, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
+  } else {
+    pp_epilogue<EPI, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
+  }
+}
 
 // ABL: ablation / A-B builds for profiling only (1-8, 16, 64, 128: wrong results): 1 no LDS-DMA in the
 // loop, 2 fragments read only in each tile's first K-tile, 4 no barriers in the loop, 8 no epilogue stores;
@@ -670,7 +687,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
       } else {
         int m0, n0;
         coords(first + (lt - 1) * G, m0, n0);
-        pp_epilogue<EPI, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
+        pp_epilogue_any<EPI, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
       }
       // the accumulators are free only after the epilogue has read them: keep the fragment reads
       // (96 VGPRs) from being hoisted into it
@@ -722,7 +739,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
   if constexpr ((ABL & 8) == 0) {
     int m0, n0;
     coords(first + (my_tiles - 1) * G, m0, n0);
-    pp_epilogue<EPI, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
+    pp_epilogue_any<EPI, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
   }
   if (g == 0 && !(ABL & 4)) bar();  // group 1 ran one barrier more
   if constexpr (Q != 0) {  // one amax partial per wave (vector atomic on an ordered-int view)

@@ -28,6 +28,7 @@ import torch
 
 from .. import ops
 from ..config import LlamaConfig
+from ..ops.cross_entropy import LM_KEY
 from .param_store import ParamStore
 
 _WARNED = set()
@@ -287,10 +288,12 @@ class LlamaForCausalLM:
                 # layer i+1's gradients are final once the backward of the add+norm that produces its
                 # input (and owns its input_layernorm weight) has run: hook that norm's input
                 m = _GradHook.apply(m, hook, i + 1)
-            q = self._q8(f"{i + 1}.qkv") if i + 1 < L else None
+            q = self._q8(f"{i + 1}.qkv") if i + 1 < L else self._q8(LM_KEY)
             y, h = ops.add_rmsnorm(h, m, self._m(nxt), self._g(nxt), eps, cdt, q8=q,
                                    q8_bwd=self._q8(f"{i}.down", grad=True))
             y8 = q.out if q is not None else None
+        # the final norm's fused e4m3 copy of y feeds the fp8 lm head (ops/cross_entropy.py); None otherwise
+        self._lm_y8 = y8 if L > 0 else None
         return y
 
     def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None, attention_mask=None,
@@ -306,8 +309,12 @@ class LlamaForCausalLM:
             if targets is None:
                 targets = ops.reference.shift_labels(labels, ops.IGNORE_INDEX)
             w_lm = self._w(lm)
+            f8 = None
+            if self._fp8_on(LM_KEY) and self.training and torch.is_grad_enabled():
+                f8 = (self.fp8, self.store.version, getattr(self, "_lm_y8", None))
             out.loss = ops.lm_head_ce(y, w_lm, self._g(lm), targets.reshape(-1), loss_scale,
-                                      wt=self._wt("lm_head", w_lm))
+                                      wt=self._wt("lm_head", w_lm) if f8 is None else None, f8=f8)
+            self._lm_y8 = None
         if return_logits or (labels is None and targets is None):
             with torch.no_grad():
                 B, T = input_ids.shape

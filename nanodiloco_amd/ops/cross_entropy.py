@@ -13,7 +13,11 @@ chunks; for each chunk:
   4. ``gW += dlogits^T @ y_c``         (wgrad, fp32 accumulate into the flat grad buffer)
 
 so only one chunk of logits ever exists and nothing [N, V]-sized survives the forward.
-``s = loss_scale / n_valid`` is read from device memory (no host sync).  The returned loss is the
+``s = loss_scale / n_valid`` is read from device memory (no host sync).
+
+fp8 (``f8`` = the model's ``Fp8Linears``, BASELINE config 5): the three GEMMs run on the own fp8 kernels --
+logits = e4m3 y8 . W8^T, the CE kernel's bf16 dlogits are cast once to e5m2 (delayed scaling, slot
+"x.lm"), dy = dlogits8 . (W^T)8^T and gW += dlogits8^T y8 (wgrad8_pp_kernel).  The returned loss is the
 unscaled mean over valid tokens (ignore_index=-100), matching ``HF/loss/loss_utils.py:32-71``.
 
 Contract: the weight gradient is produced in the forward, assuming the loss is back-propagated
@@ -45,7 +49,7 @@ def _chunk_rows(V: int, elem: int, budget_bytes: int = 0) -> int:
 
 class LMHeadCEFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, w, gw, targets, loss_scale, chunk_rows, wt):
+    def forward(ctx, y, w, gw, targets, loss_scale, chunk_rows, wt, f8=None):
         n, d = y.shape
         V = w.shape[0]
         targets = targets.reshape(-1)
@@ -56,6 +60,18 @@ class LMHeadCEFn(torch.autograd.Function):
         loss_sum = torch.zeros(1, dtype=torch.float32, device=y.device)
         hip = _ext.use_hip(y)
         det = deterministic()
+        q = None
+        if f8 is not None and hip:
+            from .fp8 import E4M3, E5M2, _wgrad_f8, cast
+            from .gemm import gemm_pp_f8, pp_f8_supported
+            lin, version, y8 = f8
+            kx, kdy = lin._slots(LM_KEY)
+            r = lin.recipe
+            if y8 is None or y8.shape != y.shape:
+                y8 = r.quantize(y, kx, E4M3)
+            wq = lin.weights[LM_KEY].get(w, version)
+            if pp_f8_supported(y8, wq.w8) and V % 128 == 0:
+                q = (r, kx, kdy, y8, wq)
         chunk = chunk_rows or _chunk_rows(V, y.element_size() if hip else 4)
         if not chunk_rows and n > chunk:  # equal-sized chunks: one GEMM shape, one tuned kernel
             nch = -(-n // chunk)
@@ -64,7 +80,11 @@ class LMHeadCEFn(torch.autograd.Function):
             e = min(n, s + chunk)
             yc, tc = y[s:e], targets[s:e]
             if hip:
-                logits = mm_nt(yc, w)  # own projection GEMM (ops/linear.py proj_gemm), hipBLASLt as fallback
+                if q is not None:  # fp8: e4m3 x e4m3 on the own fp8 ping-pong kernel
+                    r, kx, kdy, y8, wq = q
+                    logits = gemm_pp_f8(y8[s:e], wq.w8, r.inv[kx:kx + 1], wq.inv)
+                else:  # the selected plain projection GEMM (ops/linear.py proj_gemm: hipBLASLt by default)
+                    logits = mm_nt(yc, w)
                 rows = torch.empty(e - s, dtype=torch.float32, device=y.device) if det else None
                 _ext.check(_ext.lib().nd_ce_fwd_bwd(_ext.ptr(logits), _ext.dtcode(logits), _ext.ptr(tc),
                                                     _ext.ptr(loss_sum), _ext.ptr(scale), e - s, V, IGNORE_INDEX,
@@ -84,6 +104,15 @@ class LMHeadCEFn(torch.autograd.Function):
                 p.scatter_add_(1, tgt[:, None], -torch.ones_like(p[:, :1]))
                 p *= ok[:, None].to(p.dtype) * scale
                 dl = p.to(y.dtype)
+            if q is not None:
+                # e5m2 dlogits (one cast; delayed scaling of slot kdy), then both gradient GEMMs in fp8
+                r, kx, kdy, y8, wq = q
+                r._first_use(dl, kdy)
+                dl8 = cast(dl, r.scale[kdy:kdy + 1], E5M2, r.amax[kdy])
+                gemm_pp_f8(dl8, wq.wT8, r.inv[kdy:kdy + 1], wq.inv, out=dy[s:e])
+                if gw is not None:
+                    _wgrad_f8(gw, dl8, y8[s:e], r.inv[kdy:kdy + 1], r.inv[kx:kx + 1], dl)
+                continue
             # dy rows written in place (a row slice of a contiguous tensor); with wt = W^T the GEMM
             # has the faster K-contiguous operand layout (ops/linear.py)
             if wt is not None and dl.dtype == wt.dtype:
@@ -102,10 +131,14 @@ class LMHeadCEFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (dy,) = ctx.saved_tensors
-        return dy * g.to(dy.dtype), None, None, None, None, None, None
+        return dy * g.to(dy.dtype), None, None, None, None, None, None, None
+
+
+LM_KEY = "x.lm"  # the lm head's slot pair / weight cache in Fp8Linears (ops/fp8.py fp8_projection("lm"))
 
 
 def lm_head_ce(y: torch.Tensor, w: torch.Tensor, gw: torch.Tensor, targets: torch.Tensor,
-               loss_scale: float = 1.0, chunk_rows: int = 0, wt: torch.Tensor = None) -> torch.Tensor:
-    """``wt``: optional W^T copy [d, V] for the input-gradient GEMM (see ops/linear.py)."""
-    return LMHeadCEFn.apply(y, w, gw, targets, float(loss_scale), int(chunk_rows), wt)
+               loss_scale: float = 1.0, chunk_rows: int = 0, wt: torch.Tensor = None, f8=None) -> torch.Tensor:
+    """``wt``: optional W^T copy [d, V] for the input-gradient GEMM (see ops/linear.py).  ``f8``:
+    (Fp8Linears, weight version, fused e4m3 copy of y or None) for the fp8 lm head."""
+    return LMHeadCEFn.apply(y, w, gw, targets, float(loss_scale), int(chunk_rows), wt, f8)

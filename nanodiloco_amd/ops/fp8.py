@@ -110,8 +110,23 @@ def fp8_keep_fused() -> dict:
     return dict(_KEEP)
 
 
+# the lm head under --fp8: e4m3 logits GEMM, e5m2 dlogits for its input / weight gradients, all on the own
+# fp8 kernels (ops/cross_entropy.py) -- no library GEMM left in the fp8 step; False: the bf16 lm head
+_LM = {"enabled": True}
+
+
+def set_fp8_lm_head(enabled: bool) -> None:
+    _LM["enabled"] = bool(enabled)
+
+
+def fp8_lm_head() -> bool:
+    return _LM["enabled"]
+
+
 def fp8_projection(kind: str) -> bool:
-    """Whether decoder projection ``kind`` (qkv / o / gu / down) runs in fp8 under --fp8."""
+    """Whether projection ``kind`` (qkv / o / gu / down; lm = the lm head) runs in fp8 under --fp8."""
+    if kind == "lm":
+        return _LM["enabled"]
     if kind == "qkv":
         return not _KEEP["rope"]
     if kind in ("gu", "down"):

@@ -289,3 +289,29 @@ def test_fp8_fused_epilogues_track_unfused():
     u, f = losses[False], losses[True]
     assert f[-1] < 0.5 * f[0], f
     assert abs(f[-1] - u[-1]) < 0.1 * u[0], (u[-1], f[-1])
+
+
+def test_fp8_lm_head_tracks_bf16_one_step():
+    """The fp8 lm head (e4m3 logits GEMM, e5m2 dlogits into the fp8 dgrad / wgrad kernels, ops/cross_entropy.py)
+    against the bf16 one on the same weights: loss, input gradient and weight gradient within fp8 tolerance."""
+    from nanodiloco_amd.ops.cross_entropy import lm_head_ce
+    torch.manual_seed(0)
+    n, d, V = 1024, 256, 1024
+    y = (torch.randn(n, d, device="cuda") * 0.5).bfloat16().requires_grad_(True)
+    w = (torch.randn(V, d, device="cuda") * 0.05).bfloat16()
+    t = torch.randint(0, V, (n,), device="cuda")
+    res = {}
+    for use in (False, True):
+        gw = torch.zeros(V, d, device="cuda")
+        f8 = (fp8.Fp8Linears("cuda", wgrad_fp8=True), 0, None) if use else None
+        yy = y.detach().clone().requires_grad_(True)
+        loss = lm_head_ce(yy, w, gw, t, 1.0, f8=f8)
+        loss.backward()
+        from nanodiloco_amd.ops.linear import join_wgrad
+        join_wgrad()
+        torch.cuda.synchronize()
+        res[use] = (loss.item(), yy.grad.float(), gw)
+    (lb, gb, wb), (lf, gf, wf) = res[False], res[True]
+    rel = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+    assert abs(lf - lb) < 0.01 * lb, (lf, lb)
+    assert rel(gf, gb) < 0.15 and rel(wf, wb) < 0.15, (rel(gf, gb), rel(wf, wb))
