@@ -12,7 +12,11 @@ Directory layout (written only at outer-step boundaries, when all replicas are i
 With ``--overlap-outer`` a checkpoint taken at an outer boundary holds that step still PENDING (its
 all-reduce finished, its one-step-late application not yet done): the reduced pseudo-gradient and each
 rank's drift base and local weights go into the rank files, and the resumed run applies the step after its first inner
-step -- the same trajectory as the uninterrupted run (tests/test_e2e_cpu.py).
+step -- the same trajectory as the uninterrupted run (tests/test_e2e_cpu.py).  Such an INTERMEDIATE checkpoint is
+not export-ready: its model.safetensors holds rank 0's local weights (drifted by that worker's inner progress,
+without the pending outer update), and config.json says so (``"nanodiloco_pending_outer_step": true``).  For
+evaluation / export use a checkpoint without that flag -- the final one (``Diloco.finalize`` applies the
+pending step first) or any checkpoint of a run without ``--overlap-outer``.
 
 Only safetensors + JSON: nothing executable is ever deserialised.
 """
@@ -70,8 +74,11 @@ def save_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, step: int, data_
     with open(os.path.join(ckpt_dir, f"rank{r}.json"), "w") as f:
         json.dump(scal, f)
     if r == 0:
+        cfg_json = model.config.to_hf_json()
+        if pending is not None:  # see the module doc: weights are rank 0's local ones, not the synced model
+            cfg_json["nanodiloco_pending_outer_step"] = True
         with open(os.path.join(ckpt_dir, "config.json"), "w") as f:
-            json.dump(model.config.to_hf_json(), f, indent=2)
+            json.dump(cfg_json, f, indent=2)
         _save_st(os.path.join(ckpt_dir, "model.safetensors"), {n: store.master_view(n) for n in store.names})
         sync = diloco.sync.to(store.device) if diloco.sync.device != store.device else diloco.sync
         _save_st(os.path.join(ckpt_dir, "diloco_state.safetensors"),

@@ -81,6 +81,7 @@ def test_resume_matches_uninterrupted(tmp_path, nproc, inner_dp, overlap):
     assert [x["step"] for x in rb] == [5, 6]
     if overlap:
         assert json.load(open(b / "trainer_state.json"))["pending_outer"] is False  # final save: applied
+        assert "nanodiloco_pending_outer_step" not in json.load(open(b / "config.json"))  # export-ready
     assert ra[-1]["loss"] == rb[-1]["loss"]
     for f in ("model.safetensors", "diloco_state.safetensors"):
         ta, tb = _tensors(a / f), _tensors(b / f)

@@ -315,3 +315,65 @@ def test_fp8_lm_head_tracks_bf16_one_step():
     rel = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
     assert abs(lf - lb) < 0.01 * lb, (lf, lb)
     assert rel(gf, gb) < 0.15 and rel(wf, wb) < 0.15, (rel(gf, gb), rel(wf, wb))
+
+
+def _fp8_model_steps(cfg, ids, steps, overlap=None, fused=None):
+    """A few fp8 training steps (fp8 weight gradients); returns (per-step flat grads, final master weights)."""
+    from nanodiloco_amd.ops import linear as L
+    prev_ov = L.wgrad_overlap_enabled()
+    try:
+        if overlap is not None:
+            ops.set_wgrad_overlap(overlap)
+        if fused is not None:
+            fp8.set_fp8_fused_epilogues(fused)
+        m = LlamaForCausalLM(cfg, "cuda", torch.bfloat16, fp8=True, fp8_wgrad=True).init_weights(11)
+        opt = FlatAdamW(m.store, lr=2e-3)
+        grads = []
+        for _ in range(steps):
+            out = m(ids, labels=ids)
+            out.loss.backward()
+            L.join_wgrad()
+            grads.append(m.store.grad.clone())
+            opt.step()
+            m.fp8.recipe.update()
+            m.store.zero_grad()
+        torch.cuda.synchronize()
+        return grads, m.store.master.clone(), m
+    finally:
+        ops.set_wgrad_overlap(prev_ov)
+        fp8.set_fp8_fused_epilogues(True)
+
+
+def test_fp8_wgrad_side_stream_matches_serial():
+    """fp8 weight gradients on the side stream (the trainer default: fp8_wgrad + wgrad_overlap) against the
+    serial schedule: the same own kernels, so gradients and weights are bitwise equal (advisor r4)."""
+    cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=768, num_attention_heads=4,
+                                     num_key_value_heads=4, num_hidden_layers=2, vocab_size=512))
+    ids = torch.randint(0, 512, (8, 256), device="cuda")
+    ops.set_deterministic(True)
+    try:
+        g0, p0, _ = _fp8_model_steps(cfg, ids, 3, overlap=0)
+        g1, p1, m = _fp8_model_steps(cfg, ids, 3, overlap=1)
+    finally:
+        ops.set_deterministic(False)
+    for a, b in zip(g0, g1):
+        assert torch.equal(a, b)
+    assert torch.equal(p0, p1)
+
+
+def test_fp8_fused_epilogue_gradients_match_unfused_one_step():
+    """One step, same weights and (first-use) fp8 scales: the fused RoPE / SwiGLU / SwiGLU-backward fp8 GEMMs
+    give the unfused path's parameter gradients within fp8 rounding -- a wrong RoPE or SwiGLU backward (e.g. a
+    gradient that is never un-rotated) is O(1) off (advisor r4)."""
+    cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=768, num_attention_heads=4,
+                                     num_key_value_heads=4, num_hidden_layers=2, vocab_size=512))
+    ids = torch.randint(0, 512, (8, 256), device="cuda")
+    gu, _, mu = _fp8_model_steps(cfg, ids, 1, overlap=0, fused=False)
+    gf, _, mf = _fp8_model_steps(cfg, ids, 1, overlap=0, fused=True)
+    a, b = gf[0], gu[0]
+    assert ((a - b).norm() / b.norm()).item() < 3e-2
+    for name in ("model.layers.0.self_attn.q_proj.weight", "model.layers.1.self_attn.k_proj.weight",
+                 "model.layers.0.mlp.gate_proj.weight", "model.layers.1.mlp.up_proj.weight",
+                 "model.layers.0.mlp.down_proj.weight", "model.embed_tokens.weight"):
+        x, y = mf.store._view(a, name), mu.store._view(b, name)
+        assert ((x - y).norm() / y.norm()).item() < 5e-2, name
