@@ -1,7 +1,8 @@
 """Projection GEMMs with gradient routing into the flat fp32 grad buffer.
 
-``y = x @ W^T`` for W of shape [out, in].  Forward and dgrad are plain library GEMMs
-(hipBLASLt through ``torch.mm``).  The weight gradient is accumulated straight into the fp32
+``y = x @ W^T`` for W of shape [out, in].  Plain forward and dgrad products go to the selected plain GEMM
+(``set_proj_gemm``: hipBLASLt through ``torch.mm`` by default, or the own kernels); the fused ones
+(``LinearRopeFn``, ``MLPFn``) always run on the own kernel.  The weight gradient is accumulated straight into the fp32
 ``ParamStore.grad`` view: bf16 operands, fp32 accumulate, beta=1 -- one GEMM, no bf16 grad
 tensor, no separate accumulate pass.  On the HIP path that GEMM is our own ``nd_wgrad`` kernel
 (ops/gemm.py); otherwise hipBLASLt ``addmm(out_dtype=fp32)`` (this replaces autograd's per-parameter AccumulateGrad,
@@ -128,18 +129,17 @@ def wgrad_accumulate(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor):
 
 
 # ---- which GEMM runs the PLAIN projection products (forward / input gradient, lm head)
-#   "blas" hipBLASLt through torch.mm -- the default: the own kernel reaches 0.94-1.01x of it per
-#          shape (profiles/r3_gemm_pp.md) and the step is 1.5 % faster this way
+#   "blas" hipBLASLt through torch.mm -- the default: over the ten plain Llama-150M products the own kernels
+#          reach 0.924x (pp) / 0.920x (w128) of it per shape, and the bf16 step is 1.9 % (pp) / 3.2 % (w128)
+#          slower with them (round 5, gpurun_out r5a / r5k; profiles/r5_gemm.md); the task brief allows a
+#          library for PLAIN GEMMs -- every fused product and every weight gradient is on the own kernels
 #   "pp"   own ping-pong MFMA kernel (csrc/gemm_pp.hip; ops.gemm.gemm_pp) for every projection
-#   "short" own kernel for the short-K products (K <= 1024: o forward / dgrad, lm-head logits), where it
-#          is at parity per shape; hipBLASLt for the long-K dgrads (0.90x there)
-#   "w128" own one-wave-per-SIMD kernel (csrc/gemm_w128.hip: hipBLASLt's K-loop shape, 128 x 128 per
-#          wave): 0.93-0.95x hipBLASLt per shape (profiles/r4_gemm_w128.md), ahead of "pp" on the long-K
-#          products (lm-head dgrad 0.91x vs 0.87x)
+#   "short" own kernel for the short-K products (K <= 1024: o forward / dgrad, lm-head logits); hipBLASLt for
+#          the long-K dgrads (0.86-0.94x there)
+#   "w128" own one-wave-per-SIMD kernel (csrc/gemm_w128.hip: hipBLASLt's K-loop shape, 128 x 128 per wave)
 # The FUSED products always run on the own kernel (they exist only there): RoPE in the q|k|v
 # projection's epilogue, SwiGLU in the gate|up projection's, the SwiGLU backward in the down
-# projection's dgrad -- on by default (+0.8 % end to end over hipBLASLt + separate kernels,
-# +2.3 % on the own kernel; profiles/r3_gemm_pp.md).
+# projection's dgrad.  Under --fp8 every product (lm head included) runs on the own fp8 kernel.
 _PROJ = {"gemm": "blas", "rope": True, "mlp": True}
 
 

@@ -319,8 +319,7 @@ def test_fp8_lm_head_tracks_bf16_one_step():
 
 def _fp8_model_steps(cfg, ids, steps, overlap=None, fused=None):
     """A few fp8 training steps (fp8 weight gradients); returns (per-step flat grads, final master weights)."""
-    from nanodiloco_amd.ops import linear as L
-    prev_ov = L.wgrad_overlap_enabled()
+    prev_ov = ops.wgrad_overlap_enabled()
     try:
         if overlap is not None:
             ops.set_wgrad_overlap(overlap)
@@ -332,7 +331,7 @@ def _fp8_model_steps(cfg, ids, steps, overlap=None, fused=None):
         for _ in range(steps):
             out = m(ids, labels=ids)
             out.loss.backward()
-            L.join_wgrad()
+            ops.join_wgrad()
             grads.append(m.store.grad.clone())
             opt.step()
             m.fp8.recipe.update()
@@ -362,18 +361,26 @@ def test_fp8_wgrad_side_stream_matches_serial():
 
 
 def test_fp8_fused_epilogue_gradients_match_unfused_one_step():
-    """One step, same weights and (first-use) fp8 scales: the fused RoPE / SwiGLU / SwiGLU-backward fp8 GEMMs
-    give the unfused path's parameter gradients within fp8 rounding -- a wrong RoPE or SwiGLU backward (e.g. a
-    gradient that is never un-rotated) is O(1) off (advisor r4)."""
+    """One step, same weights: the fused RoPE / SwiGLU / SwiGLU-backward fp8 GEMMs give parameter gradients as
+    close to the bf16 model's as the unfused fp8 path does (per tensor, within 1.5x of its deviation) -- a wrong
+    RoPE or SwiGLU backward (e.g. a gradient that is never un-rotated) lands O(1) away (advisor r4)."""
     cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=768, num_attention_heads=4,
                                      num_key_value_heads=4, num_hidden_layers=2, vocab_size=512))
     ids = torch.randint(0, 512, (8, 256), device="cuda")
     gu, _, mu = _fp8_model_steps(cfg, ids, 1, overlap=0, fused=False)
     gf, _, mf = _fp8_model_steps(cfg, ids, 1, overlap=0, fused=True)
-    a, b = gf[0], gu[0]
-    assert ((a - b).norm() / b.norm()).item() < 3e-2
-    for name in ("model.layers.0.self_attn.q_proj.weight", "model.layers.1.self_attn.k_proj.weight",
-                 "model.layers.0.mlp.gate_proj.weight", "model.layers.1.mlp.up_proj.weight",
-                 "model.layers.0.mlp.down_proj.weight", "model.embed_tokens.weight"):
-        x, y = mf.store._view(a, name), mu.store._view(b, name)
-        assert ((x - y).norm() / y.norm()).item() < 5e-2, name
+    mb = LlamaForCausalLM(cfg, "cuda", torch.bfloat16).init_weights(11)
+    mb(ids, labels=ids).loss.backward()
+    ops.join_wgrad()
+    torch.cuda.synchronize()
+    gb = mb.store.grad
+    rel = lambda x, y: ((x - y).norm() / y.norm().clamp_min(1e-20)).item()  # noqa: E731
+    rows = []
+    for name in mb.store.names:
+        if "norm" in name:
+            continue
+        f, u, b = mf.store._view(gf[0], name), mu.store._view(gu[0], name), mb.store._view(gb, name)
+        rows.append((name, rel(f, b), rel(u, b), rel(f, u)))
+    print("\n".join(f"{n:45s} fused~bf16 {x:.3f} unfused~bf16 {y:.3f} fused~unfused {z:.3f}" for n, x, y, z in rows))
+    for n, x, y, z in rows:
+        assert x < 1.5 * y + 0.02 and x < 0.5, (n, x, y, z)
