@@ -72,6 +72,8 @@ def parse():
                     help="issue weight-gradient GEMMs on a side HIP stream (overlaps the dgrad chain), joined "
                          "before every hipBLASLt GEMM (1, default: +0.4 %% per step, "
                          "profiles/r4_wgrad_overlap_ab.md); 0 off; 2 unfenced (A/B only)")
+    ap.add_argument("--wgrad-group", type=int, default=1, choices=[0, 1],
+                    help="the MLP's down and gate|up weight gradients as one grouped own-kernel launch (1, default)")
     ap.add_argument("--wgrad-variant", default=None,
                     help="ND_WGRAD_VARIANT for the weight-gradient kernel (A/B of kernel schedules)")
     ap.add_argument("--attn-fused-stats", type=int, default=1, choices=[0, 1],
@@ -137,6 +139,7 @@ def main():
     tr = Trainer(targs)
     env, cfg, dl = tr.env, tr.llama_config, tr.diloco
     ops.set_wgrad_overlap(a.wgrad_overlap)  # mode 2 (unfenced A/B) is not a trainer option
+    ops.set_wgrad_group(bool(a.wgrad_group))
     if env.world_size != a.gpus and env.rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
     if env.device.type == "cuda" and a.tuned_gemm_file:
@@ -252,6 +255,7 @@ def main():
             "final_loss": round(final_loss, 4),
             "tuned_gemm": enable_tuned_gemms(env.device) if env.device.type == "cuda" and not a.no_tuned_gemm else False,
             "wgrad_overlap": ops.wgrad_overlap_enabled(),
+            "wgrad_group": ops.wgrad_group_enabled(),
             "proj_gemm": ops.proj_gemm(),
             "fused_epilogues": ops.fused_epilogues(),
             "fp8_gemm": a.fp8_gemm if a.fp8 else None,

@@ -686,17 +686,38 @@ __device__ __forceinline__ void wpp_vmn(int n) {  // n in {0, 4, 8}
 }
 }  // namespace
 
+// One weight-gradient product of a (possibly grouped) launch: C[M, N] (+)= A^T B, A [K, M], B [K, N].
+struct WgProb {
+  const bf16_t* A;
+  const bf16_t* B;
+  float* C;
+  float* slab;
+  int M, N;
+  int64_t lda, ldb, ldc;
+};
+
 // ABL (timing ablations, wrong results; ND_WGRAD_VARIANT=a<bits>): 1 no LDS-DMA in the loop, 2 fragments read
 // only for the first K-tile, 4 no barriers in the loop, 8 no vmcnt waits in the loop, 16 no MFMAs
+//
+// Grouped launch (round 5): workgroups [0, nwg0) run product p0, the rest p1 (same K and split count S).
+// Two products whose tile counts alone leave CUs idle fill the chip together: the Llama-150M MLP's
+// down (44 tiles) and gate|up (84) weight gradients are 220 + 252 workgroups as separate launches
+// (S = 5 / 3) but exactly 256 as one launch with S = 2.
 template <bool GD, int ABL = 0>
-__global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                                          float* __restrict__ C, float* __restrict__ slab, int M, int N,
-                                                          int K, int64_t lda, int64_t ldb, int64_t ldc, int S, int kchunk) {
+__global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(WgProb p0, WgProb p1, int nwg0, int K, int S, int kchunk) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem_bf[];
   char* smem = reinterpret_cast<char*>(smem_bf);
+  const int gid = xcd_remap(blockIdx.x, gridDim.x);
+  const bool second = gid >= nwg0;
+  const bf16_t* __restrict__ A = second ? p1.A : p0.A;
+  const bf16_t* __restrict__ B = second ? p1.B : p0.B;
+  float* __restrict__ C = second ? p1.C : p0.C;
+  float* __restrict__ slab = second ? p1.slab : p0.slab;
+  const int M = second ? p1.M : p0.M, N = second ? p1.N : p0.N;
+  const int64_t lda = second ? p1.lda : p0.lda, ldb = second ? p1.ldb : p0.ldb, ldc = second ? p1.ldc : p0.ldc;
   const int tn_count = (N + 255) / 256;
   const int tiles = ((M + 255) / 256) * tn_count;
-  const int id = xcd_remap(blockIdx.x, tiles * S);
+  const int id = second ? gid - nwg0 : gid;
   const int split = id / tiles, tile = id % tiles;
   const int m0 = (tile / tn_count) * 256, n0 = (tile % tn_count) * 256;
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
@@ -1099,13 +1120,14 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
                      hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<true>),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (attrp != hipSuccess) return (int)attrp;
+    const WgProb prob{(const bf16_t*)A, (const bf16_t*)B, C, slab, M, N, lda, ldb, ldc};
 #ifdef ND_ABLATION
     if (ev && ev[0] == 'a') {  // timing ablations (wrong results)
       const int abl = atoi(ev + 1);
 #define ND_WA(X) case X: hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<true, X>), \
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-  hipLaunchKernelGGL((wgrad_pp_kernel<true, X>), dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, \
-                     (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk); break;
+  hipLaunchKernelGGL((wgrad_pp_kernel<true, X>), dim3(tiles * S), dim3(512), lds, s, prob, prob, tiles * S, K, S, \
+                     kchunk); break;
       switch (abl) { ND_WA(1) ND_WA(2) ND_WA(4) ND_WA(8) ND_WA(16) ND_WA(3) ND_WA(7) ND_WA(15) ND_WA(31) default: return (int)hipErrorInvalidValue; }
 #undef ND_WA
       ND_LAUNCH_CHECK();
@@ -1114,11 +1136,9 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
     // default: full half-tiles staged with FLAT-global LDS loads (bitwise the same as the buffer form,
     // 1.005x over the three Llama-150M shapes, profiles/r4_gdma_ab.md); "b": buffer loads only (A/B)
     if (!(ev && ev[0] == 'b'))
-      hipLaunchKernelGGL(wgrad_pp_kernel<true>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
-                         C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
+      hipLaunchKernelGGL(wgrad_pp_kernel<true>, dim3(tiles * S), dim3(512), lds, s, prob, prob, tiles * S, K, S, kchunk);
     else
-      hipLaunchKernelGGL(wgrad_pp_kernel<false>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
-                         C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
+      hipLaunchKernelGGL(wgrad_pp_kernel<false>, dim3(tiles * S), dim3(512), lds, s, prob, prob, tiles * S, K, S, kchunk);
   } else if (large && variant == 5 && M >= 8 && N >= 8 && K % BK3 == 0) {  // "4w": 4-wave, AGPR-pinned accumulators
     const int kchunk = fit_kchunk(K, &S, BK3);
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
@@ -1171,6 +1191,79 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
     int64_t blocks = ((int64_t)M * N / 4 + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, slab, C, M, N, ldc, S);
+  }
+  ND_LAUNCH_CHECK();
+}
+
+// ---- grouped weight gradients: two products with the same K (tokens) in ONE ping-pong launch.
+// The split count is chosen for the pair: the estimated makespan ceil(T S / CUs) * ceil(nk / S) K-tiles
+// plus the slab traffic of S > 1 (written once, read once by slab_reduce_kernel, ~5 TB/s), in units of
+// one K-tile of one workgroup (~1.8 us at the measured 1.2 PF/s).
+static int num_cus_wg() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      return 256;
+    return v;
+  }();
+  return n;
+}
+
+static bool wgrad_pp_eligible(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
+  return M % 8 == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 && K % 64 == 0 && K > 0 &&
+         ((M + 255) / 256) * ((N + 255) / 256) >= 8 && (int64_t)64 * (lda > ldb ? lda : ldb) * 2 < (1ll << 31);
+}
+
+static int group_splits(int T, int K, int64_t mn_total) {
+  const int nk = K / 64, ncu = num_cus_wg();
+  int best = 1;
+  double best_cost = 1e300;
+  for (int S = 1; S <= 16; ++S) {
+    if (S > 1 && nk / S < 4) break;
+    const double waves = (double)((T * S + ncu - 1) / ncu);
+    const double cost = waves * (double)((nk + S - 1) / S) + (S > 1 ? (double)(S + 2) * mn_total * 4.0 / 8.95e6 : 0.0);
+    if (cost < best_cost * 0.999) {
+      best_cost = cost;
+      best = S;
+    }
+  }
+  return best;
+}
+
+// Split count of the grouped launch, or 0 when the pair cannot be grouped (then call nd_wgrad twice).
+// Slab workspace: S * M0 * N0 floats for product 0 and S * M1 * N1 for product 1 (S > 1).
+ND_API int nd_wgrad2_splits(int M0, int N0, int M1, int N1, int K) {
+  const char* ev = wgrad_env();
+  if ((ev && ev[0]) || !wgrad_pp_eligible(M0, N0, K, 8, 8, 4) || !wgrad_pp_eligible(M1, N1, K, 8, 8, 4)) return 0;
+  const int T = ((M0 + 255) / 256) * ((N0 + 255) / 256) + ((M1 + 255) / 256) * ((N1 + 255) / 256);
+  return group_splits(T, K, (int64_t)M0 * N0 + (int64_t)M1 * N1);
+}
+
+ND_API int nd_wgrad2(const void* A0, const void* B0, float* C0, float* slab0, int M0, int N0, int64_t lda0, int64_t ldb0,
+                     int64_t ldc0, const void* A1, const void* B1, float* C1, float* slab1, int M1, int N1, int64_t lda1,
+                     int64_t ldb1, int64_t ldc1, int K, hipStream_t s) {
+  int S = nd_wgrad2_splits(M0, N0, M1, N1, K);
+  if (S <= 0 || !wgrad_pp_eligible(M0, N0, K, lda0, ldb0, ldc0) || !wgrad_pp_eligible(M1, N1, K, lda1, ldb1, ldc1))
+    return (int)hipErrorInvalidValue;
+  if (S > 1 && (slab0 == nullptr || slab1 == nullptr)) return (int)hipErrorInvalidValue;
+  const int kchunk = fit_kchunk(K, &S, 64);  // may only lower S: the caller's slabs stay large enough
+  const int T0 = ((M0 + 255) / 256) * ((N0 + 255) / 256), T1 = ((M1 + 255) / 256) * ((N1 + 255) / 256);
+  const size_t lds = 2 * (size_t)WPP_BUF_B;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<true>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return (int)attr;
+  const WgProb p0{(const bf16_t*)A0, (const bf16_t*)B0, C0, slab0, M0, N0, lda0, ldb0, ldc0};
+  const WgProb p1{(const bf16_t*)A1, (const bf16_t*)B1, C1, slab1, M1, N1, lda1, ldb1, ldc1};
+  hipLaunchKernelGGL(wgrad_pp_kernel<true>, dim3((T0 + T1) * S), dim3(512), lds, s, p0, p1, T0 * S, K, S, kchunk);
+  if (S > 1) {
+    const WgProb* ps[2] = {&p0, &p1};
+    for (const WgProb* p : ps) {
+      int64_t blocks = ((int64_t)p->M * p->N / 4 + 255) / 256;
+      if (blocks > 4096) blocks = 4096;
+      hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p->slab, p->C, p->M, p->N, p->ldc,
+                         S);
+    }
   }
   ND_LAUNCH_CHECK();
 }

@@ -190,6 +190,8 @@ def _declare(L: ctypes.CDLL):
         # weight-gradient GEMM
         "nd_wgrad_splits": [I, I, I],
         "nd_wgrad": [P, P, P, P, I, I, I, L64, L64, L64, P],
+        "nd_wgrad2_splits": [I, I, I, I, I],
+        "nd_wgrad2": [P, P, P, P, I, I, L64, L64, L64, P, P, P, P, I, I, L64, L64, L64, I, P],
     }
     for name, argtypes in sigs.items():
         fn = getattr(L, name, None)

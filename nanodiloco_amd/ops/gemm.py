@@ -243,6 +243,33 @@ def wgrad(gw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
                           gw.stride(0), _ext.stream_ptr(gw.device)), "nd_wgrad")
 
 
+def wgrad2(gw0: torch.Tensor, dy0: torch.Tensor, x0: torch.Tensor,
+           gw1: torch.Tensor, dy1: torch.Tensor, x1: torch.Tensor) -> bool:
+    """Both weight gradients ``gw_i += dy_i^T x_i`` (same token count K) in ONE ping-pong launch whose split
+    count is chosen for the pair (csrc/gemm_wgrad.hip nd_wgrad2): e.g. the Llama-150M MLP's down (44 tiles)
+    and gate|up (84 tiles) products fill exactly 256 CUs together with 2 K-splits, where alone they leave
+    36 / 4 CUs idle.  Returns False (nothing issued) when the pair cannot be grouped -- the caller then
+    runs ``wgrad`` twice."""
+    K, M0 = dy0.shape
+    N0, M1, N1 = x0.shape[1], dy1.shape[1], x1.shape[1]
+    if dy1.shape[0] != K or x0.shape[0] != K or x1.shape[0] != K:
+        return False
+    if tuple(gw0.shape) != (M0, N0) or tuple(gw1.shape) != (M1, N1):
+        return False
+    L = _ext.lib()
+    S = L.nd_wgrad2_splits(M0, N0, M1, N1, K)
+    if S <= 0:
+        return False
+    ws0 = ws1 = None
+    if S > 1:
+        ws = _workspace(gw0.device, S * (M0 * N0 + M1 * N1))
+        ws0, ws1 = ws, ws[S * M0 * N0:]
+    _ext.check(L.nd_wgrad2(_ext.ptr(dy0), _ext.ptr(x0), _ext.ptr(gw0), _ext.ptr(ws0), M0, N0, dy0.stride(0),
+                           x0.stride(0), gw0.stride(0), _ext.ptr(dy1), _ext.ptr(x1), _ext.ptr(gw1), _ext.ptr(ws1), M1,
+                           N1, dy1.stride(0), x1.stride(0), gw1.stride(0), K, _ext.stream_ptr(gw0.device)), "nd_wgrad2")
+    return True
+
+
 def wgrad_f8_supported(gw: torch.Tensor, dy8: torch.Tensor, x8: torch.Tensor) -> bool:
     """Can ``wgrad_f8`` run: fp8 token-major operands (dy e4m3 / e5m2, x e4m3), tokens % 128, M, N >= 256."""
     return (gw.is_cuda and _ext.get_backend() != "torch" and gw.dtype == torch.float32 and dy8.dim() == 2

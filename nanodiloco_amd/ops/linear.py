@@ -194,6 +194,46 @@ def _wgrad(gw, dy, x):
         wgrad_accumulate(gw, dy, x)
 
 
+# Grouped weight gradients (round 5): the MLP's down and gate|up weight gradients as ONE own-kernel launch
+# (ops.gemm.wgrad2), issued after the gate|up input-gradient GEMM instead of one before and one after it.
+_GROUP = {"enabled": True}
+
+
+def set_wgrad_group(enabled: bool) -> None:
+    _GROUP["enabled"] = bool(enabled)
+
+
+def wgrad_group_enabled() -> bool:
+    return _GROUP["enabled"]
+
+
+def wgrad2_accumulate(gw0, dy0, x0, gw1, dy1, x1) -> None:
+    """gw0 += dy0^T x0 and gw1 += dy1^T x1, grouped into one launch when the own kernel takes both."""
+    if (gw0.is_cuda and _ext.get_backend() != "torch" and dy0.dtype == torch.bfloat16 and dy1.dtype == torch.bfloat16):
+        from .gemm import wgrad2, wgrad_supported
+        if wgrad_supported(gw0, dy0, x0) and wgrad_supported(gw1, dy1, x1) and wgrad2(gw0, dy0, x0, gw1, dy1, x1):
+            return
+    wgrad_accumulate(gw0, dy0, x0)
+    wgrad_accumulate(gw1, dy1, x1)
+
+
+def _wgrad2(gw0, dy0, x0, gw1, dy1, x1):
+    if gw0 is None or gw1 is None:
+        _wgrad(gw0, dy0, x0)
+        _wgrad(gw1, dy1, x1)
+        return
+    if _OVERLAP["enabled"] and gw0.is_cuda:
+        cur = torch.cuda.current_stream(gw0.device)
+        side = _side_stream(gw0.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            wgrad2_accumulate(gw0, dy0, x0, gw1, dy1, x1)
+        _OVERLAP["keep"].append((dy0, x0, dy1, x1))
+        _OVERLAP["pending"].add(side.device.index)
+    else:
+        wgrad2_accumulate(gw0, dy0, x0, gw1, dy1, x1)
+
+
 class LinearFn(torch.autograd.Function):
     """``wt`` (optional) is W^T stored [in, out] contiguous: the input gradient is then dY . (W^T)^T,
     the same K-contiguous "NT" operand layout as the forward GEMM, which hipBLASLt runs 14-16 %
@@ -295,6 +335,10 @@ class MLPFn(torch.autograd.Function):
         gw_gu, gw_down = ctx.gw
         dm = dm.contiguous()
         dgu = gemm_pp_dswiglu(dm, wt_down, gu)
+        if _GROUP["enabled"]:  # both weight gradients in one launch, after the input gradient
+            dy = mm_nt(dgu, wt_gu) if ctx.needs_input_grad[0] else None
+            _wgrad2(gw_down, dm, act, gw_gu, dgu, y)
+            return dy, None, None, None, None, None, None
         _wgrad(gw_down, dm, act)
         dy = mm_nt(dgu, wt_gu) if ctx.needs_input_grad[0] else None
         _wgrad(gw_gu, dgu, y)

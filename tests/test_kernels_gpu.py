@@ -289,6 +289,46 @@ def test_wgrad_no_empty_split_with_poisoned_slabs(variant, monkeypatch):
     assert rel(gw, dy.float().t() @ x.float()) < 1e-5
 
 
+@pytest.mark.parametrize("shapes,K", [(((1024, 2688), (5376, 1024)), 16384),   # Llama-150M down + gate|up
+                                      (((3072, 1024), (1024, 1024)), 8192),    # q|k|v + o
+                                      (((2048, 5632), (11264, 2048)), 4096),   # Llama-1B down + gate|up
+                                      (((1000, 1032), (520, 2048)), 41 * 64)])  # partial tiles, K tail
+def test_wgrad_grouped(shapes, K):
+    """Two weight gradients in one grouped launch (nd_wgrad2) against fp32 references; run twice with
+    NaN-poisoned slabs in between (deterministic, no stale slab plane summed)."""
+    from nanodiloco_amd.ops import gemm as G
+    (M0, N0), (M1, N1) = shapes
+    dy0, x0 = torch.randn(K, M0, device=DEV).bfloat16(), torch.randn(K, N0, device=DEV).bfloat16()
+    dy1, x1 = torch.randn(K, M1, device=DEV).bfloat16(), torch.randn(K, N1, device=DEV).bfloat16()
+    g0, g1 = torch.randn(M0, N0, device=DEV), torch.randn(M1, N1, device=DEV)
+    r0, r1 = g0 + dy0.float().t() @ x0.float(), g1 + dy1.float().t() @ x1.float()
+    outs = []
+    for _ in range(2):
+        G._workspace(torch.device(DEV), 16 * (M0 * N0 + M1 * N1)).fill_(float("nan"))
+        a0, a1 = g0.clone(), g1.clone()
+        assert G.wgrad2(a0, dy0, x0, a1, dy1, x1)
+        assert rel(a0, r0) < 1e-5 and rel(a1, r1) < 1e-5, (rel(a0, r0), rel(a1, r1))
+        outs.append((a0, a1))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    S = ext_lib().nd_wgrad2_splits(M0, N0, M1, N1, K)
+    if shapes[0] == (1024, 2688) and K == 16384:
+        assert S == 2, S  # 44 + 84 tiles: 256 workgroups
+
+
+def test_wgrad_grouped_refuses_mismatch():
+    from nanodiloco_amd.ops import gemm as G
+    dy0, x0 = torch.randn(512, 1024, device=DEV).bfloat16(), torch.randn(512, 1024, device=DEV).bfloat16()
+    dy1, x1 = torch.randn(256, 1024, device=DEV).bfloat16(), torch.randn(256, 1024, device=DEV).bfloat16()
+    g = torch.zeros(1024, 1024, device=DEV)
+    assert not G.wgrad2(g, dy0, x0, g.clone(), dy1, x1)  # different K: not grouped, nothing issued
+    assert g.abs().max().item() == 0
+
+
+def ext_lib():
+    from nanodiloco_amd.ops import _ext
+    return _ext.lib()
+
+
 def test_wgrad_strided_views():
     """Operands that are column slices of a wider buffer (fused q|k|v grads)."""
     from nanodiloco_amd.ops.gemm import wgrad
