@@ -1037,6 +1037,49 @@ __global__ void __launch_bounds__(512, 1) wgrad8_pp_kernel(const uint8_t* __rest
   }
 }
 
+// ND_WGRAD_PLAN=old: the fixed split rule only (A/B of the makespan model)
+static const bool g_wgrad_plan_cost = [] {
+  const char* e = getenv("ND_WGRAD_PLAN");
+  return !(e && e[0] == 'o');
+}();
+
+static int num_cus_wg() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      return 256;
+    return v;
+  }();
+  return n;
+}
+
+static bool wgrad_pp_eligible(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
+  return M % 8 == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 && K % 64 == 0 && K > 0 &&
+         ((M + 255) / 256) * ((N + 255) / 256) >= 8 && (int64_t)64 * (lda > ldb ? lda : ldb) * 2 < (1ll << 31);
+}
+
+static double split_cost(int T, int K, int64_t mn_total, int S) {
+  const int nk = K / 64, ncu = num_cus_wg();
+  const double waves = (double)((T * S + ncu - 1) / ncu);
+  return waves * (double)((nk + S - 1) / S) + (S > 1 ? (double)(S + 2) * mn_total * 4.0 / 8.95e6 : 0.0);
+}
+
+static int group_splits(int T, int K, int64_t mn_total) {
+  const int nk = K / 64;
+  int best = 1;
+  double best_cost = 1e300;
+  for (int S = 1; S <= 16; ++S) {
+    if (S > 1 && nk / S < 4) break;
+    const double cost = split_cost(T, K, mn_total, S);
+    if (cost < best_cost * 0.999) {
+      best_cost = cost;
+      best = S;
+    }
+  }
+  return best;
+}
+
 static int splits_for(int tiles, int K, int bk, int target) {
   int S = target / tiles;
   if (S < 1) S = 1;
@@ -1047,10 +1090,20 @@ static int splits_for(int tiles, int K, int bk, int target) {
 
 // Variant choice: the 256 x 256 kernel (1 workgroup / CU) when the output has >= 8 such tiles,
 // else the 128 x 128 kernel.  Returns splits * 2 + (large ? 1 : 0) so the caller can size the slab.
-static int plan(int M, int N, int K, int* S_out) {
+static int plan(int M, int N, int K, int* S_out, bool use_cost = true) {
   const int t256 = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
   if (t256 >= 8) {
-    *S_out = splits_for(t256, K, BK2, 256);
+    int S = splits_for(t256, K, BK2, 256);
+    // the makespan model of the grouped launch, taken only when it predicts >= 10 % (idle CUs clock the
+    // busy ones up, so small predicted gains do not materialise: profiles/r5_gemm_tokens.md); e.g. the
+    // Llama-1B down-projection gradient: 176 tiles -> S = 4 instead of 176 workgroups on 256 CUs (bf16
+    // step +1.7 %).  Not for the fp8 kernel (use_cost = false): its side-stream wgrads share the chip with
+    // unfenced own GEMMs, and the 1B fp8 step measured 0.973x with the model
+    if (use_cost && g_wgrad_plan_cost && K % 64 == 0) {
+      const int Sc = group_splits(t256, K, (int64_t)M * N);
+      if (split_cost(t256, K, (int64_t)M * N, Sc) < 0.9 * split_cost(t256, K, (int64_t)M * N, S)) S = Sc;
+    }
+    *S_out = S;
     return 1;
   }
   const int t128 = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
@@ -1086,6 +1139,13 @@ static const char* wgrad_env() {
 ND_API int nd_wgrad_splits(int M, int N, int K) {
   int S;
   plan(M, N, K, &S);
+  return S;
+}
+
+// The same for the fp8 weight-gradient kernel (nd_wgrad_f8).
+ND_API int nd_wgrad_f8_splits(int M, int N, int K) {
+  int S;
+  plan(M, N, K, &S, false);
   return S;
 }
 
@@ -1199,45 +1259,21 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
 // The split count is chosen for the pair: the estimated makespan ceil(T S / CUs) * ceil(nk / S) K-tiles
 // plus the slab traffic of S > 1 (written once, read once by slab_reduce_kernel, ~5 TB/s), in units of
 // one K-tile of one workgroup (~1.8 us at the measured 1.2 PF/s).
-static int num_cus_wg() {
-  static int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-      return 256;
-    return v;
-  }();
-  return n;
-}
-
-static bool wgrad_pp_eligible(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
-  return M % 8 == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 && K % 64 == 0 && K > 0 &&
-         ((M + 255) / 256) * ((N + 255) / 256) >= 8 && (int64_t)64 * (lda > ldb ? lda : ldb) * 2 < (1ll << 31);
-}
-
-static int group_splits(int T, int K, int64_t mn_total) {
-  const int nk = K / 64, ncu = num_cus_wg();
-  int best = 1;
-  double best_cost = 1e300;
-  for (int S = 1; S <= 16; ++S) {
-    if (S > 1 && nk / S < 4) break;
-    const double waves = (double)((T * S + ncu - 1) / ncu);
-    const double cost = waves * (double)((nk + S - 1) / S) + (S > 1 ? (double)(S + 2) * mn_total * 4.0 / 8.95e6 : 0.0);
-    if (cost < best_cost * 0.999) {
-      best_cost = cost;
-      best = S;
-    }
-  }
-  return best;
-}
-
 // Split count of the grouped launch, or 0 when the pair cannot be grouped (then call nd_wgrad twice).
 // Slab workspace: S * M0 * N0 floats for product 0 and S * M1 * N1 for product 1 (S > 1).
 ND_API int nd_wgrad2_splits(int M0, int N0, int M1, int N1, int K) {
   const char* ev = wgrad_env();
   if ((ev && ev[0]) || !wgrad_pp_eligible(M0, N0, K, 8, 8, 4) || !wgrad_pp_eligible(M1, N1, K, 8, 8, 4)) return 0;
-  const int T = ((M0 + 255) / 256) * ((N0 + 255) / 256) + ((M1 + 255) / 256) * ((N1 + 255) / 256);
-  return group_splits(T, K, (int64_t)M0 * N0 + (int64_t)M1 * N1);
+  const int T0 = ((M0 + 255) / 256) * ((N0 + 255) / 256), T1 = ((M1 + 255) / 256) * ((N1 + 255) / 256);
+  const int64_t mn = (int64_t)M0 * N0 + (int64_t)M1 * N1;
+  const int S = group_splits(T0 + T1, K, mn);
+  // group only when the model predicts a clear win over the two separate launches (each with its own plan):
+  // Llama-150M down + gate|up 1039 vs 1114 K-tile units (grouped); Llama-1B 1241 vs 1208 (separate)
+  int S0, S1;
+  plan(M0, N0, K, &S0);
+  plan(M1, N1, K, &S1);
+  const double sep = split_cost(T0, K, (int64_t)M0 * N0, S0) + split_cost(T1, K, (int64_t)M1 * N1, S1);
+  return split_cost(T0 + T1, K, mn, S) < 0.97 * sep ? S : 0;
 }
 
 ND_API int nd_wgrad2(const void* A0, const void* B0, float* C0, float* slab0, int M0, int N0, int64_t lda0, int64_t ldb0,
@@ -1277,7 +1313,7 @@ ND_API int nd_wgrad_f8(const void* A, const void* B, float* C, float* slab, int 
       (fa != 0 && fa != 1) || (int64_t)128 * (lda > ldb ? lda : ldb) >= (1ll << 31))
     return (int)hipErrorInvalidValue;
   int S;
-  plan(M, N, K, &S);
+  plan(M, N, K, &S, false);
   if (S > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
   const int kchunk = fit_kchunk(K, &S, 128);
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);

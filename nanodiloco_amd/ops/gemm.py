@@ -288,7 +288,7 @@ def wgrad_f8(gw: torch.Tensor, dy8: torch.Tensor, x8: torch.Tensor, s_dy: torch.
     N = x8.shape[1]
     assert x8.shape[0] == K and tuple(gw.shape) == (M, N)
     L = _ext.lib()
-    S = L.nd_wgrad_splits(M, N, K)
+    S = L.nd_wgrad_f8_splits(M, N, K)
     ws = _workspace(gw.device, S * M * N) if S > 1 else None
     _ext.check(L.nd_wgrad_f8(_ext.ptr(dy8), _ext.ptr(x8), _ext.ptr(gw), _ext.ptr(ws), M, N, K, dy8.stride(0),
                              x8.stride(0), gw.stride(0), _ext.ptr(s_dy), _ext.ptr(s_x), _F8_FMT[dy8.dtype],

@@ -291,7 +291,7 @@ def test_wgrad_no_empty_split_with_poisoned_slabs(variant, monkeypatch):
 
 @pytest.mark.parametrize("shapes,K", [(((1024, 2688), (5376, 1024)), 16384),   # Llama-150M down + gate|up
                                       (((3072, 1024), (1024, 1024)), 8192),    # q|k|v + o
-                                      (((2048, 5632), (11264, 2048)), 4096),   # Llama-1B down + gate|up
+                                      (((2048, 5632), (11264, 2048)), 4096),   # Llama-1B down + gate|up (not grouped)
                                       (((1000, 1032), (520, 2048)), 41 * 64)])  # partial tiles, K tail
 def test_wgrad_grouped(shapes, K):
     """Two weight gradients in one grouped launch (nd_wgrad2) against fp32 references; run twice with
@@ -302,6 +302,12 @@ def test_wgrad_grouped(shapes, K):
     dy1, x1 = torch.randn(K, M1, device=DEV).bfloat16(), torch.randn(K, N1, device=DEV).bfloat16()
     g0, g1 = torch.randn(M0, N0, device=DEV), torch.randn(M1, N1, device=DEV)
     r0, r1 = g0 + dy0.float().t() @ x0.float(), g1 + dy1.float().t() @ x1.float()
+    S = ext_lib().nd_wgrad2_splits(M0, N0, M1, N1, K)
+    if S == 0:  # the makespan model prefers two launches (Llama-1B MLP): nothing issued
+        a0 = g0.clone()
+        assert not G.wgrad2(a0, dy0, x0, g1.clone(), dy1, x1)
+        assert torch.equal(a0, g0)
+        return
     outs = []
     for _ in range(2):
         G._workspace(torch.device(DEV), 16 * (M0 * N0 + M1 * N1)).fill_(float("nan"))
@@ -310,7 +316,6 @@ def test_wgrad_grouped(shapes, K):
         assert rel(a0, r0) < 1e-5 and rel(a1, r1) < 1e-5, (rel(a0, r0), rel(a1, r1))
         outs.append((a0, a1))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    S = ext_lib().nd_wgrad2_splits(M0, N0, M1, N1, K)
     if shapes[0] == (1024, 2688) and K == 16384:
         assert S == 2, S  # 44 + 84 tiles: 256 workgroups
 
