@@ -306,8 +306,9 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
             u2[j][r] = rbf(F8 != 0 ? acc[a][j + 2][r] * sc : acc[a][j + 2][r]);
             y2[j][r] = silu(g2[j][r]) * u2[j][r];
           }
-        const uint32_t og = ok ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
-        const uint32_t ou = ok ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
+        const bool okst = ok && (ABL & 8192) == 0;  // ABL 8192: stores out of range (no HBM writes; timing only)
+        const uint32_t og = okst ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
+        const uint32_t ou = okst ? (uint32_t)(((int64_t)mr * ldc + N + f) * 2) : 0x80000000u;
         __builtin_amdgcn_raw_buffer_store_b128(pair16(g2[0], g2[1]), cr, og, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(pair16(u2[0], u2[1]), cr, ou, 0, 0);
         if constexpr (Q != 0) {
@@ -329,7 +330,7 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
           const uint32_t oq = ok ? (uint32_t)((int64_t)mr * ep.ld_q8 + f) : 0x80000000u;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, o), qr, oq, 0, 0);
         } else {
-          const uint32_t oy = ok ? (uint32_t)(((int64_t)mr * ep.ld_act + f) * 2) : 0x80000000u;
+          const uint32_t oy = okst ? (uint32_t)(((int64_t)mr * ep.ld_act + f) * 2) : 0x80000000u;
           __builtin_amdgcn_raw_buffer_store_b128(pair16(y2[0], y2[1]), ar, oy, 0, 0);
         }
       }
@@ -351,6 +352,11 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
       };
 #pragma unroll
       for (int st = 0; st < PF; ++st) {
+        if constexpr ((ABL & 4096) != 0) {  // ablation: no gate / up loads (wrong result)
+          gq[st] = u32x4{(uint32_t)lane, 1u, 2u, 3u};
+          uq[st] = u32x4{3u, 2u, 1u, (uint32_t)lane};
+          continue;
+        }
         gq[st] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st, 0), 0, 0);
         uq[st] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st, 1), 0, 0);
       }
@@ -365,7 +371,7 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
           const bool ok = f < N;
           const int st = 2 * a + bp;
           const u32x4 gv = gq[st % PF], uv = uq[st % PF];
-          if (st + PF < 16) {
+          if (st + PF < 16 && (ABL & 4096) == 0) {
             gq[st % PF] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st + PF, 0), 0, 0);
             uq[st % PF] = __builtin_amdgcn_raw_buffer_load_b128(gr, gu_off(st + PF, 1), 0, 0);
           }
@@ -433,8 +439,9 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
                   const int rr = i * 8 + ((lane + z) >> 3);  // staging row: i < 2 gate, else up
                   const u32x4 d = *reinterpret_cast<const u32x4*>(stg + rr * 128 + ((lc ^ (rr & 7)) << 4));
                   const int grow = g * 128 + a * 16 + (rr & 15);
-                  const uint32_t off =
-                      col < N ? (uint32_t)(((int64_t)grow * ldc + (i >= 2 ? N : 0) + col) * 2) : 0x80000000u;
+                  const uint32_t off = col < N && (ABL & 8192) == 0
+                                           ? (uint32_t)(((int64_t)grow * ldc + (i >= 2 ? N : 0) + col) * 2)
+                                           : 0x80000000u;
                   __builtin_amdgcn_raw_buffer_store_b128(d, cr, off, 0, STP);
                 }
                 asm volatile("" ::: "memory");
@@ -800,6 +807,13 @@ template <int EPI, int HD = 64>
 int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
               const PPEpi& ep, hipStream_t s) {
   if (g_pp_variant == 1024) return launch_pp_v<EPI, HD, 1024>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+#ifdef ND_ABLATION
+  if constexpr (EPI == PP_DSWIGLU || EPI == PP_SWIGLU) {  // epilogue ablations of the fused MLP products
+    if (g_pp_variant == 8) return launch_pp_v<EPI, HD, 8>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    if (g_pp_variant == 4096) return launch_pp_v<EPI, HD, 4096>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    if (g_pp_variant == 8192) return launch_pp_v<EPI, HD, 8192>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+  }
+#endif
   if constexpr (EPI == PP_STORE) {
     switch (g_pp_variant) {
 #ifdef ND_ABLATION
