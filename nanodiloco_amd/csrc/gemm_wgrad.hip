@@ -17,6 +17,7 @@
 // Tile: 128 x 128 per 256-thread workgroup (2 x 2 waves of 64 x 64, 2 x 2 v_mfma_f32_32x32x16_bf16).
 #include "common.h"
 #include <cstdlib>
+#include <cstring>
 
 
 using namespace nd;
@@ -147,10 +148,9 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(const bf16_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------------
-// Large-tile variant: 256 x 256 per 512-thread workgroup (8 waves as 2 (M) x 4 (N), 128 x 64 each =
-// 4 x 2 MFMA tiles), BK = 32, DOUBLE-BUFFERED LDS with one barrier per K tile:
-//   compute(buf[k&1]) | global loads of tile k+2 in flight | write tile k+1 regs -> buf[(k+1)&1] | barrier
-// 1.5 transposing LDS reads per MFMA (vs 2 in the 128 x 128 kernel), 16 MFMAs per wave per barrier.
+// 256 x 256 tile geometry and the transposing fragment helpers of the LDS-DMA kernel below (8 waves as
+// 2 (M) x 4 (N), 128 x 64 each).  (The round-2 register-staged 256 x 256 kernel and the round-3 4-wave
+// AGPR variant that used to sit here measured slower than the ping-pong kernel; removed in round 5.)
 namespace {
 constexpr int BM2 = 256, BN2 = 256, BK2 = 32;
 
@@ -170,113 +170,11 @@ __device__ __forceinline__ bf16x8 frag2(const bf16_t* tile, int kbase, int cbase
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
 }
-
-struct TileLoad2 {  // BK2 x 256 bf16 = 1024 16-B chunks over 512 threads
-  bf16x8 v[2];
-  __device__ __forceinline__ void load(const bf16_t* base, int64_t ld, int k0, int kend, int c0, int cols) {
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int c = threadIdx.x + it * 512;
-      const int row = c >> 5, ch = c & 31;
-      const int k = k0 + row, col = c0 + ch * 8;
-      if (k < kend && col < cols) v[it] = *reinterpret_cast<const bf16x8*>(base + (int64_t)k * ld + col);
-      else v[it] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
-  }
-  __device__ __forceinline__ void store(bf16_t* tile) const {
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int c = threadIdx.x + it * 512;
-      const int row = c >> 5, ch = c & 31;
-      *reinterpret_cast<bf16x8*>(&tile[toff2(row, ch * 8)]) = v[it];
-    }
-  }
-};
 }  // namespace
 
-__global__ void __launch_bounds__(512, 2) wgrad256_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                                          float* __restrict__ C, float* __restrict__ slab, int M, int N,
-                                                          int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
-                                                          int kchunk) {
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  // buffer b: A at smem + b * BK2 * BM2, B at smem + 2 * BK2 * BM2 + b * BK2 * BN2
-  const int tn_count = (N + BN2 - 1) / BN2;
-  const int tiles = ((M + BM2 - 1) / BM2) * tn_count;
-  const int id = xcd_remap(blockIdx.x, tiles * S);
-  const int split = id / tiles, tile = id % tiles;  // one XCD: same K range, neighbouring tiles (L2 reuse)
-  const int m0 = (tile / tn_count) * BM2, n0 = (tile % tn_count) * BN2;
-  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int g = lane >> 4, i16 = lane & 15;
-  const int wm = w >> 2, wn = w & 3;  // 2 x 4 waves, wave tile 128 (M) x 64 (N)
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
-
-  const int nk = (kend - kbeg + BK2 - 1) / BK2;
-  TileLoad2 la, lb;
-  if (nk > 0) {
-    la.load(A, lda, kbeg, kend, m0, M);
-    lb.load(B, ldb, kbeg, kend, n0, N);
-    la.store(smem);
-    lb.store(smem + 2 * BK2 * BM2);
-  }
-  __syncthreads();
-  if (nk > 1) {
-    la.load(A, lda, kbeg + BK2, kend, m0, M);
-    lb.load(B, ldb, kbeg + BK2, kend, n0, N);
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    const bf16_t* a_t = smem + (kt & 1) * BK2 * BM2;
-    const bf16_t* b_t = smem + 2 * BK2 * BM2 + (kt & 1) * BK2 * BN2;
-#pragma unroll
-    for (int ks = 0; ks < BK2 / 16; ++ks) {
-      bf16x8 fb[2];
-#pragma unroll
-      for (int b = 0; b < 2; ++b) fb[b] = frag2(b_t, ks * 16, wn * 64 + b * 32, g, i16);
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const bf16x8 fa = frag2(a_t, ks * 16, wm * 128 + a * 32, g, i16);
-#pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(fa, fb[b], acc[a][b]);
-      }
-    }
-    if (kt + 1 < nk) {
-      la.store(smem + ((kt + 1) & 1) * BK2 * BM2);
-      lb.store(smem + 2 * BK2 * BM2 + ((kt + 1) & 1) * BK2 * BN2);
-    }
-    __syncthreads();
-    if (kt + 2 < nk) {
-      la.load(A, lda, kbeg + (kt + 2) * BK2, kend, m0, M);
-      lb.load(B, ldb, kbeg + (kt + 2) * BK2, kend, n0, N);
-    }
-  }
-  float* out = S == 1 ? C : slab + (int64_t)split * M * N;
-  const int64_t ldo = S == 1 ? ldc : N;
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int n = n0 + wn * 64 + b * 32 + c32;
-      if (n >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < M) {
-          float* p = out + (int64_t)m * ldo + n;
-          if (S == 1) *p += acc[a][b][r];
-          else *p = acc[a][b][r];
-        }
-      }
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
-// LDS-DMA variant (the production path): same 256 x 256 / 8-wave / 128 x 64-per-wave geometry, but
-// tiles move global -> LDS with global_load_lds_dwordx4 (no VGPR round trip, no ds_write issue cost,
+// LDS-DMA kernel (round 2; since round 3 the path for K % 64 != 0 and the dma0 / dmas A/B variants): same
+// 256 x 256 / 8-wave / 128 x 64-per-wave geometry, but tiles move global -> LDS with global_load_lds_dwordx4 (no VGPR round trip, no ds_write issue cost,
 // which bounded the register-staged kernel).  The LDS image is lane-linear per wave-instruction
 // (1 KiB = two 512-B rows), so the bank swizzle is applied on the SOURCE address: the lane that
 // lands in physical chunk p of row r loads logical chunk p ^ ((r & 3) << 2), and the transposing
@@ -450,155 +348,6 @@ __global__ void __launch_bounds__(512, 2) wgrad_dma_kernel(const bf16_t* __restr
 
 
 
-
-// ---------------------------------------------------------------------------------------------
-// 4-wave variant (ND_WGRAD_VARIANT=4w; same 256 x 256 tile, LDS image and split-K plan): each wave
-// owns a 128 x 128 quadrant = 4 x 4 v_mfma_f32_32x32x16_bf16 accumulators (256 AGPRs), one wave per
-// SIMD.  The MFMAs are inline asm with tied "+a" accumulators (hipcc would otherwise shuffle a
-// 256-register accumulator set through VGPR copies: csrc/gemm.hip), 16 transposing fragment reads
-// per 16 MFMAs (vs 12 per 8 with the 8-wave split), and the LDS-DMA pieces of tile k+2 are issued
-// between the MFMAs of k-step 3 of tile k and k-step 0 of tile k+1 instead of as one burst.
-// K-tile schedule (4 k-steps of 16): ks0..ks2 read the next k-step's fragments under their MFMAs;
-// after ks2 one vmcnt(0) + barrier (tile k+1 landed everywhere, buffer k&1 read by everyone);
-// ks3 reads tile k+1's ks0 fragments.
-namespace {
-__device__ __forceinline__ void mfma32a(const bf16x8& a, const bf16x8& b, f32x16& c) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void mfma32_drain() { asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 3" ::: "memory"); }
-
-}  // namespace
-
-__global__ void __launch_bounds__(256, 1) wgrad4_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                                        float* __restrict__ C, float* __restrict__ slab, int M, int N,
-                                                        int K, int64_t lda, int64_t ldb, int64_t ldc, int S,
-                                                        int kchunk) {
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  constexpr int TA = BK3 * BM2, TB = BK3 * BN2;  // elements per operand tile
-  const int tn_count = (N + BN2 - 1) / BN2;
-  const int tiles = ((M + BM2 - 1) / BM2) * tn_count;
-  const int id = xcd_remap(blockIdx.x, tiles * S);
-  const int split = id / tiles, tile = id % tiles;
-  const int m0 = (tile / tn_count) * BM2, n0 = (tile % tn_count) * BN2;
-  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int g = lane >> 4, i16 = lane & 15;
-  const int wm = w >> 1, wn = w & 1;  // 2 x 2 waves, 128 x 128 each
-  const int wr = __builtin_amdgcn_readfirstlane(w);
-
-  f32x16 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x16{};
-
-  const int nk = kend > kbeg ? (kend - kbeg + BK3 - 1) / BK3 : 0;
-  // per-lane DMA offsets: wave w moves row pairs w + 4 it (it = 0..7) of each 64 x 256 operand tile;
-  // (row & 3) == (2 w + rp) & 3 for every it, so one swizzled column per lane serves all pieces
-  const int rp = lane >> 5;
-  const int csw = (lane & 31) ^ (((2 * w + rp) & 3) << 2);
-  int cola = m0 + csw * 8, colb = n0 + csw * 8;
-  cola = cola < M ? cola : M - 8;
-  colb = colb < N ? colb : N - 8;
-  const uint32_t va = (uint32_t)(((int64_t)rp * lda + cola) * 2);
-  const uint32_t vb = (uint32_t)(((int64_t)rp * ldb + colb) * 2);
-  const uint32_t lds_base = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) bf16_t*)smem);
-  // piece j (0-7: A pair w + 4j, 8-15: B pair w + 4(j - 8)) of full tile kt into its buffer
-  auto piece = [&](int kt, int j) __attribute__((always_inline)) {
-    const int k0 = kbeg + kt * BK3;
-    const uint32_t tb = lds_base + (uint32_t)((kt & 1) * (TA + TB) * 2);
-    const int pr = wr + 4 * (j & 7);
-    if (j < 8) glds16s(A + (int64_t)(k0 + 2 * pr) * lda, va, tb + (uint32_t)(pr * 1024));
-    else glds16s(B + (int64_t)(k0 + 2 * pr) * ldb, vb, tb + (uint32_t)(TA * 2 + pr * 1024));
-  };
-  // host guarantees K % 64 == 0 (and kchunk % 64 == 0): every tile is full, streamed by LDS-DMA
-  auto stage_all = [&](int kt) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) piece(kt, j);
-  };
-  if (nk == 0) return;  // (S is planned so every split has work; nothing to write otherwise)
-  stage_all(0);
-  if (nk > 1) stage_all(1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  bf16x8 fa0[4], fb0[4], fa1[4], fb1[4];
-  auto rd = [&](const bf16_t* a_t, const bf16_t* b_t, int ks, bf16x8* fa, bf16x8* fb, int i) __attribute__((always_inline)) {
-    fb[i] = frag2(b_t, ks * 16, wn * 128 + i * 32, g, i16);
-    fa[i] = frag2(a_t, ks * 16, wm * 128 + i * 32, g, i16);
-  };
-  {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rd(smem, smem + TA, 0, fa0, fb0, i);
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    const bf16_t* a_t = smem + (kt & 1) * (TA + TB);
-    const bf16_t* b_t = a_t + TA;
-    const bool dma2 = kt + 2 < nk;                   // tile kt+2: A pieces in this ks3, B pieces in the next ks0
-    const bool dma1_late = kt >= 1 && kt + 1 < nk;   // B pieces of tile kt+1 (its A pieces went in ks3 of kt-1)
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this k-step's fragments
-    // ---- ks0 (+ B pieces of tile kt+1 when it streams by DMA)
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      if (dma1_late) { piece(kt + 1, 8 + 2 * a); piece(kt + 1, 9 + 2 * a); }
-      rd(a_t, b_t, 1, fa1, fb1, a);
-#pragma unroll
-      for (int b = 0; b < 4; ++b) mfma32a(fa0[a], fb0[b], acc[a][b]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // ---- ks1
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      rd(a_t, b_t, 2, fa0, fb0, a);
-#pragma unroll
-      for (int b = 0; b < 4; ++b) mfma32a(fa1[a], fb1[b], acc[a][b]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // ---- ks2
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      rd(a_t, b_t, 3, fa1, fb1, a);
-#pragma unroll
-      for (int b = 0; b < 4; ++b) mfma32a(fa0[a], fb0[b], acc[a][b]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // tile kt+1 has landed (this wave's DMA), everyone's reads of buffer kt&1 are done
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- ks3: A pieces of tile kt+2 and tile kt+1's ks0 fragments under the MFMAs
-    const bf16_t* an = smem + ((kt + 1) & 1) * (TA + TB);
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      if (dma2) { piece(kt + 2, 2 * a); piece(kt + 2, 2 * a + 1); }
-      rd(an, an + TA, 0, fa0, fb0, a);  // past the split's end: reads unused LDS
-#pragma unroll
-      for (int b = 0; b < 4; ++b) mfma32a(fa1[a], fb1[b], acc[a][b]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  mfma32_drain();
-  float* out = S == 1 ? C : slab + (int64_t)split * M * N;
-  const int64_t ldo = S == 1 ? ldc : N;
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int n = n0 + wn * 128 + b * 32 + c32;
-      if (n >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < M) {
-          float* p = out + (int64_t)m * ldo + n;
-          if (S == 1) *p += acc[a][b][r];
-          else *p = acc[a][b][r];
-        }
-      }
-    }
-}
 
 // C[m][n] += sum_s slab[s][m][n]   (fixed summation order)
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ C, int M,
@@ -1156,21 +905,18 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
   int S;
   const int large = plan(M, N, K, &S);
   if (S > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
-  // ND_WGRAD_VARIANT (A/B runs): "reg" register-staged 256 kernel, "dmas" LDS-DMA with the
-  // sched_group_barrier interleave, "nodma" compute-only diagnostic (skips the loads: wrong result);
-  // default ("dma0"): LDS-DMA, compiler-scheduled.  (s_setprio around the MFMA clusters, both
-  // per-cluster and the static waves-4-7 form, measured +-0 e2e and were dropped.)  (Measured and dropped, see docs/DESIGN.md: a 4-deep
-  // BK=32 ring with counted vmcnt, a 16x16x32-MFMA version and a quadrant-phase pipeline -- all
-  // 3-15 % slower than this kernel on the Llama-150M shapes.)
-  // read once when the library loads (wgrad_env); wrong-result variants only in -DND_ABLATION builds
+  // ND_WGRAD_VARIANT (A/B runs, read once when the library loads): "dma0" the round-2 LDS-DMA kernel,
+  // compiler-scheduled; "dmas" the same with the sched_group_barrier interleave (MFMA / 2 transposing reads:
+  // measured 4-13 % SLOWER per kernel, -1.7 % e2e); "b" the ping-pong kernel with buffer-form pieces only;
+  // "nodma" / "a<bits>" timing ablations with wrong results (-DND_ABLATION builds only).  (Measured and
+  // dropped, see docs/DESIGN.md: s_setprio around the MFMA clusters, a 4-deep BK=32 ring with counted vmcnt,
+  // a 16x16x32-MFMA version, a quadrant-phase pipeline, the register-staged 256 x 256 kernel and the 4-wave
+  // AGPR kernel -- the last two removed in round 5.)
   const char* ev = wgrad_env();
-  const int variant = (ev && ev[0] == 'r') ? 1 : (ev && ev[0] == 'n') ? 4 : (ev && ev[0] == '4') ? 5 : 0;
-  // the sched_group_barrier interleave (MFMA / 2 transposing reads) is opt-in ("dmas"): measured
-  // 4-13 % SLOWER per kernel than the compiler's own schedule at 32k and 64k tokens, -1.7 % e2e
-  const bool sched = ev && ev[0] == 'd' && ev[3] == 's';
+  const bool sched = ev && strncmp(ev, "dmas", 4) == 0;
   const bool pp = large && M >= 8 && N >= 8 && K % 64 == 0 && (int64_t)64 * (lda > ldb ? lda : ldb) * 2 < (1ll << 31) &&
-                 !(ev && (ev[0] == 'd' || ev[0] == 'r' || ev[0] == 'n' || ev[0] == '4'));
-  if (pp) {  // default: ping-pong kernel (ND_WGRAD_VARIANT=dma0 / reg / ... select the older kernels)
+                 !(ev && (ev[0] == 'd' || ev[0] == 'n'));
+  if (pp) {  // default: ping-pong kernel (ND_WGRAD_VARIANT=dma0 / dmas select the LDS-DMA kernel)
     const int kchunk = fit_kchunk(K, &S, 64);
     const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
     const size_t lds = 2 * (size_t)WPP_BUF_B;  // 128 KiB
@@ -1199,17 +945,8 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
       hipLaunchKernelGGL(wgrad_pp_kernel<true>, dim3(tiles * S), dim3(512), lds, s, prob, prob, tiles * S, K, S, kchunk);
     else
       hipLaunchKernelGGL(wgrad_pp_kernel<false>, dim3(tiles * S), dim3(512), lds, s, prob, prob, tiles * S, K, S, kchunk);
-  } else if (large && variant == 5 && M >= 8 && N >= 8 && K % BK3 == 0) {  // "4w": 4-wave, AGPR-pinned accumulators
-    const int kchunk = fit_kchunk(K, &S, BK3);
-    const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
-    const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB
-    static const hipError_t attr4 = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad4_kernel),
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)attr4;
-    hipLaunchKernelGGL(wgrad4_kernel, dim3(tiles * S), dim3(256), lds, s, (const bf16_t*)A, (const bf16_t*)B, C, slab,
-                       M, N, K, lda, ldb, ldc, S, kchunk);
 #ifdef ND_ABLATION
-  } else if (large && variant == 4) {  // "nodma": compute-only diagnostic (wrong result)
+  } else if (large && ev && ev[0] == 'n') {  // "nodma": compute-only diagnostic (wrong result)
     const int kchunk = fit_kchunk(K, &S, BK3);
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);
@@ -1219,7 +956,7 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
     hipLaunchKernelGGL((wgrad_dma_kernel<true, true>), dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A,
                        (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
 #endif
-  } else if (large && variant != 1 && variant != 4 && M >= 8 && N >= 8) {
+  } else if (large) {  // K % 64 != 0 (register-staged K tail) or ND_WGRAD_VARIANT=dma0 / dmas
     const int kchunk = fit_kchunk(K, &S, BK3);
     const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
     const size_t lds = 2 * (size_t)BK3 * (BM2 + BN2) * sizeof(bf16_t);  // 128 KiB
@@ -1235,12 +972,6 @@ ND_API int nd_wgrad(const void* A, const void* B, float* C, float* slab, int M, 
     else
       hipLaunchKernelGGL(wgrad_dma_kernel<false>, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A,
                          (const bf16_t*)B, C, slab, M, N, K, lda, ldb, ldc, S, kchunk);
-  } else if (large) {
-    const int kchunk = fit_kchunk(K, &S, BK2);
-    const int tiles = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
-    const size_t lds = 2 * (size_t)BK2 * (BM2 + BN2) * sizeof(bf16_t);
-    hipLaunchKernelGGL(wgrad256_kernel, dim3(tiles * S), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B, C,
-                       slab, M, N, K, lda, ldb, ldc, S, kchunk);
   } else {
     const int kchunk = fit_kchunk(K, &S, BK);
     const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);

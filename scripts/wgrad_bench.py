@@ -32,7 +32,7 @@ def main():
         fl = 2.0 * M * Nn * K
         res = {}
         for rnd in range(3):
-            for v in os.environ.get("VARIANTS", "dma,dma0,reg,blas").split(","):
+            for v in os.environ.get("VARIANTS", "dma,dma0,blas").split(","):
                 if v == "blas":
                     f = lambda: torch.ops.aten.addmm.dtype_out(gw, dy.t(), x, torch.float32, beta=1, alpha=1, out=gw)
                 else:

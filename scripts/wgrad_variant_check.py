@@ -17,7 +17,7 @@ def main():
         dy = torch.randn(K, M, device="cuda").bfloat16()
         x = torch.randn(K, N, device="cuda").bfloat16()
         ref = dy.float().t() @ x.float()
-        for v in os.environ.get("VARIANTS", "dma0,dmas,reg").split(","):
+        for v in os.environ.get("VARIANTS", "dma0,dmas,b").split(","):
             os.environ["ND_WGRAD_VARIANT"] = v
             gw = torch.ones(M, N, device="cuda")
             wgrad(gw, dy, x)

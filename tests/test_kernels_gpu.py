@@ -256,7 +256,7 @@ def test_outer_nesterov_matches_torch_sgd(comm):
                                    (128, 512, 64), (5376, 1024, 65536), (1024, 2688, 16640),
                                    # Llama-1B: q|k|v, gate|up, down, lm head
                                    (2560, 2048, 8192), (11264, 2048, 4096), (2048, 5632, 4096), (32000, 2048, 2048)])
-@pytest.mark.parametrize("variant", ["", "reg", "dma0", "4w"])
+@pytest.mark.parametrize("variant", ["", "dma0", "dmas", "b"])
 def test_wgrad_gemm(M, N, K, variant, monkeypatch):
     monkeypatch.setenv("ND_WGRAD_VARIANT", variant)
     from nanodiloco_amd.ops.gemm import wgrad
@@ -272,7 +272,7 @@ def test_wgrad_gemm(M, N, K, variant, monkeypatch):
     assert torch.equal(gw, gw2)  # deterministic (no atomics)
 
 
-@pytest.mark.parametrize("variant", ["", "reg", "dma0", "4w"])
+@pytest.mark.parametrize("variant", ["", "dma0", "dmas", "b"])
 def test_wgrad_no_empty_split_with_poisoned_slabs(variant, monkeypatch):
     """K = 41 * 64 over 16 output tiles: rounding the per-split K chunk up to whole tiles would leave the
     last split empty; its slab plane must not be summed stale (the workspace is NaN-poisoned first)."""
