@@ -107,8 +107,10 @@ def _dtype(name: str, device: torch.device) -> torch.dtype:
 
 # activation budget of one micro-batch as a share of device memory, and the micro-batch token target
 # (128 x 1024 at round-3 HEAD: +0.5 % bf16 / +1.8 % --fp8 over 64 x 1024 for Llama-150M in interleaved
-# A/Bs, profiles/r3_micro_batch_ab.md; Llama-1B is memory-capped at 64 x 1024, equal to 32 x 1024)
-_AUTO_MEM_SHARE = 0.3
+# A/Bs, profiles/r3_micro_batch_ab.md).  Round 5: 45 % of the 288 GB (was 30 %) so Llama-1B gets 64 x 1024
+# (~100 GB of activations) instead of 32 x 1024: +0.45 % bf16 with the makespan-planned weight-gradient splits
+# (session r5an); optimizer state and flat buffers of the 1B model take < 30 GB
+_AUTO_MEM_SHARE = 0.45
 _AUTO_TOKENS = 131072
 
 
