@@ -158,10 +158,19 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
             kw["device_id"] = dev  # eager RCCL communicator init
             kw["pg_options"] = _pg_options(backend, high_priority)
         launched = "TORCHELASTIC_RUN_ID" in os.environ and "MASTER_PORT" in os.environ
+        restart = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0)
         if world == 1 and not launched:
             # one rank outside torchrun: nothing to rendezvous with (a stray MASTER_ADDR without
             # MASTER_PORT / RANK must not send us into an env:// rendezvous)
             kw.update(store=dist.HashStore(), rank=0, world_size=1)
+        elif launched and restart > 0 and os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true":
+            # a torchrun --max-restarts restart: the static rendezvous keeps the agent's ONE TCPStore across
+            # attempts, while torch's env:// handler assumes a fresh store per attempt and adds no prefix
+            # (rendezvous._create_c10d_store), so the restarted workers would read attempt 0's keys (gloo
+            # peer addresses: "Connection refused").  Prefix this attempt's keys.
+            base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world, False,
+                                 timeout=timeout)
+            kw.update(store=dist.PrefixStore(f"nd_restart_{restart}", base), rank=rank, world_size=world)
         dist.init_process_group(**kw)
     env.backend = backend
     env.comm_impl = _resolve_comm_impl(comm_impl, backend)

@@ -83,7 +83,7 @@ class TrainArgs:
     checkpoint_dir: Optional[str] = None
     checkpoint_every: int = 0      # in outer steps (0 = only at the end when checkpoint_dir is set)
     stop_at_step: int = 0          # stop early (simulated preemption) after this inner step; 0 = run to total
-    resume: Optional[str] = None
+    resume: Optional[str] = None   # a checkpoint dir, or "auto": the newest complete one in checkpoint_dir (restarts)
     log_every: int = 1
     log_file: Optional[str] = None
     wandb: str = "auto"
@@ -197,9 +197,15 @@ class Trainer:
                                device=e.device, dataset_path=a.dataset_path, tokenizer=a.tokenizer,
                                mask_pad_labels=a.mask_pad_labels)
         self.start_step = 0
-        if a.resume:
+        resume = a.resume
+        if resume == "auto":  # restart form: the newest complete checkpoint of --checkpoint-dir, else fresh
+            from .utils.checkpoint import find_checkpoint
+            resume = find_checkpoint(a.checkpoint_dir)
+            if e.rank == 0:
+                print(f"[resume auto] {'from ' + resume if resume else 'no checkpoint: fresh start'}", flush=True)
+        if resume:
             from .utils.checkpoint import load_checkpoint
-            st = load_checkpoint(a.resume, self.model, self.diloco, e)
+            st = load_checkpoint(resume, self.model, self.diloco, e)
             self.start_step = int(st["step"])
             ds = st.get("data_state")
             if ds:
@@ -210,7 +216,7 @@ class Trainer:
                                        f"cannot restore it")
                 self.data.load_state_dict(ds)
             elif hasattr(self.data, "load_state_dict"):
-                raise RuntimeError(f"checkpoint {a.resume} has no data state for rank {e.rank}; "
+                raise RuntimeError(f"checkpoint {resume} has no data state for rank {e.rank}; "
                                    f"resuming would restart the data stream")
         self.graphed = None
         hg = str(a.hip_graph).lower()
@@ -308,6 +314,7 @@ class Trainer:
                 self.save(real_step)
             if a.stop_at_step and real_step >= a.stop_at_step:
                 break
+            _maybe_inject_fault(e.rank, real_step)
         self.diloco.finalize()
         if a.checkpoint_dir and not a.stop_at_step:
             self.save(a.total_steps)
@@ -321,6 +328,33 @@ class Trainer:
         ds = self.data.state_dict() if hasattr(self.data, "state_dict") else None
         save_checkpoint(self.args.checkpoint_dir, self.model, self.diloco, self.env, step, data_state=ds,
                         extra={"run_name": self.run_name})
+
+
+def _fault_spec():
+    """``ND_FAULT_INJECT=<rank>:<step>[:hang]`` (tests / drills): that rank crashes (exit code 17) or hangs right
+    after inner step <step> -- only in the first attempt of a torchrun job (``TORCHELASTIC_RESTART_COUNT`` 0), so
+    a ``--max-restarts`` restart runs clean."""
+    v = os.environ.get("ND_FAULT_INJECT")
+    if not v or int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0) != 0:
+        return None
+    parts = v.split(":")
+    return int(parts[0]), int(parts[1]), (parts[2] if len(parts) > 2 else "crash")
+
+
+_FAULT = {"spec": None, "read": False}
+
+
+def _maybe_inject_fault(rank: int, step: int) -> None:
+    if not _FAULT["read"]:
+        _FAULT["spec"], _FAULT["read"] = _fault_spec(), True
+    f = _FAULT["spec"]
+    if f is None or f[0] != rank or f[1] != step:
+        return
+    print(f"[fault inject] rank {rank} step {step}: {f[2]}", flush=True)
+    if f[2] == "hang":
+        while True:
+            time.sleep(60)
+    os._exit(17)
 
 
 def train_model(**kwargs) -> Dict[str, Any]:

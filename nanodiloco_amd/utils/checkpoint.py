@@ -18,17 +18,57 @@ without the pending outer update), and config.json says so (``"nanodiloco_pendin
 evaluation / export use a checkpoint without that flag -- the final one (``Diloco.finalize`` applies the
 pending step first) or any checkpoint of a run without ``--overlap-outer``.
 
+Crash consistency (round 5): every rank writes into ``<dir>.tmp``; after a barrier rank 0 adds
+``COMPLETE.json`` and swaps the staging directory in (``<dir>`` -> ``<dir>.old``, ``<dir>.tmp`` -> ``<dir>``,
+then ``<dir>.old`` is removed), so a crash at any point of a save leaves the previous complete checkpoint
+readable (``find_checkpoint`` falls back to ``<dir>.old`` when the swap itself was interrupted).  ``--resume
+auto`` resumes from the newest complete checkpoint in ``--checkpoint-dir`` if there is one and starts fresh
+otherwise -- the restart form for ``torchrun --max-restarts N`` (tests/test_e2e_cpu.py
+injects a crash with ``ND_FAULT_INJECT``).
+
 Only safetensors + JSON: nothing executable is ever deserialised.
 """
 from __future__ import annotations
 
 import json
 import os
+import shutil
 from typing import Any, Dict, Optional
 
 import torch
 
 from ..parallel.dist import DistEnv, barrier
+
+
+COMPLETE = "COMPLETE.json"
+
+
+def _stage_dir(ckpt_dir: str) -> str:
+    return os.path.normpath(ckpt_dir) + ".tmp"
+
+
+def find_checkpoint(ckpt_dir: Optional[str]) -> Optional[str]:
+    """The newest COMPLETE checkpoint for ``ckpt_dir`` (itself, or ``<dir>.old`` when a save was interrupted
+    between its two renames), a pre-round-5 checkpoint without the marker, or None."""
+    if not ckpt_dir:
+        return None
+    d = os.path.normpath(ckpt_dir)
+    for cand in (d, d + ".old"):
+        if os.path.isfile(os.path.join(cand, COMPLETE)):
+            return cand
+    if os.path.isfile(os.path.join(d, "trainer_state.json")) and not os.path.exists(_stage_dir(d)):
+        return d  # written before the staging scheme existed
+    return None
+
+
+def _swap_in(stage: str, final: str) -> None:
+    old = final + ".old"
+    if os.path.isdir(old):
+        shutil.rmtree(old)
+    if os.path.isdir(final):
+        os.replace(final, old)
+    os.replace(stage, final)
+    shutil.rmtree(old, ignore_errors=True)
 
 
 def _save_st(path: str, tensors: Dict[str, torch.Tensor]):
@@ -52,9 +92,14 @@ def save_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, step: int, data_
         # (parallel/diloco.py, sharded outer step); gather the worker's full buffer before rank 0
         # writes it, so a resumed run restores every shard (not just shard 0)
         diloco.inner_comm.all_gather_flat(diloco.outer_optimizer.momentum_buffer, diloco.shards, env.inner_rank)
-    os.makedirs(ckpt_dir, exist_ok=True)
-    store = model.store
+    final = os.path.normpath(ckpt_dir)
+    ckpt_dir = _stage_dir(final)  # every file below goes to the staging directory
     r = env.rank
+    if r == 0:
+        shutil.rmtree(ckpt_dir, ignore_errors=True)  # leftovers of a save that crashed
+        os.makedirs(ckpt_dir)
+    barrier(env)
+    store = model.store
     # per-rank state (every rank)
     per = {"adamw.exp_avg": diloco.inner_optimizer.exp_avg, "adamw.exp_avg_sq": diloco.inner_optimizer.exp_avg_sq}
     scal: Dict[str, Any] = {"adamw_step": diloco.inner_optimizer.step_count}
@@ -89,10 +134,19 @@ def save_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, step: int, data_
                  "pending_outer": pending is not None, **(extra or {})}
         with open(os.path.join(ckpt_dir, "trainer_state.json"), "w") as f:
             json.dump(state, f, indent=2)
+    barrier(env)  # every rank's files are in the staging directory
+    if r == 0:
+        with open(os.path.join(ckpt_dir, COMPLETE), "w") as f:
+            json.dump({"step": step, "world_size": env.world_size}, f)
+        _swap_in(ckpt_dir, final)
     barrier(env)
 
 
 def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv) -> Dict[str, Any]:
+    found = find_checkpoint(ckpt_dir)
+    if found is None:
+        raise FileNotFoundError(f"no complete checkpoint at {ckpt_dir}")
+    ckpt_dir = found
     with open(os.path.join(ckpt_dir, "trainer_state.json")) as f:
         state = json.load(f)
     store = model.store

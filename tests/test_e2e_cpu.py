@@ -94,6 +94,68 @@ def test_resume_matches_uninterrupted(tmp_path, nproc, inner_dp, overlap):
         assert all(mom[i * n:(i + 1) * n].abs().sum() > 0 for i in range(inner_dp))
 
 
+def _torchrun_raw(nproc, args, tmp_path, extra_env=None, run_args=(), timeout=600):
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT, **(extra_env or {}))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), *run_args, "-m", "nanodiloco_amd"] + args
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.slow
+def test_crash_restart_resumes_bitwise(tmp_path):
+    """SURVEY §5.3 fault drill: rank 1 crashes (exit 17) after inner step 5, one outer step past the checkpoint
+    of step 4; ``torchrun --max-restarts 1`` restarts the worker group, ``--resume auto`` picks the newest
+    COMPLETE checkpoint and the job finishes bit-identical to an uninterrupted run."""
+    a, b = tmp_path / "a", tmp_path / "b"
+    common = BASE + ["--inner-steps", "2", "--data", "synthetic", "--total-steps", "8"]
+    _torchrun(2, common + ["--checkpoint-dir", str(a)], tmp_path)
+    r = _torchrun_raw(2, common + ["--checkpoint-dir", str(b), "--checkpoint-every", "1", "--resume", "auto"],
+                      tmp_path, extra_env={"ND_FAULT_INJECT": "1:5"}, run_args=("--max-restarts", "1"))
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "[fault inject] rank 1 step 5: crash" in out, out[-4000:]
+    assert "[resume auto] from" in out, out[-4000:]  # the restart resumed instead of starting over
+    assert json.load(open(b / "COMPLETE.json"))["step"] == 8
+    assert not os.path.exists(str(b) + ".tmp") and not os.path.exists(str(b) + ".old")
+    for f in ("model.safetensors", "diloco_state.safetensors"):
+        ta, tb = _tensors(a / f), _tensors(b / f)
+        for k in ta:
+            assert torch.equal(ta[k], tb[k]), (f, k)
+
+
+@pytest.mark.slow
+def test_hung_peer_fails_by_collective_timeout(tmp_path):
+    """A worker that hangs (ND_FAULT_INJECT ...:hang) makes its peer's next outer all-reduce time out after
+    --collective-timeout-s: the job fails with an error within seconds instead of hanging."""
+    import time
+    t0 = time.time()
+    r = _torchrun_raw(2, BASE + ["--inner-steps", "2", "--data", "synthetic", "--total-steps", "6",
+                                 "--collective-timeout-s", "20"],
+                      tmp_path, extra_env={"ND_FAULT_INJECT": "1:1:hang"}, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode != 0, out[-4000:]
+    assert "[fault inject] rank 1 step 1: hang" in out, out[-4000:]
+    assert time.time() - t0 < 200
+    assert "time" in out.lower(), out[-4000:]  # gloo: "Timed out ..." on the waiting rank
+
+
+def test_find_checkpoint_prefers_complete(tmp_path):
+    """Crash consistency of the staging scheme: only a directory with COMPLETE.json (or its .old copy while a
+    swap was interrupted) is a resume point; a half-written staging directory never is."""
+    from nanodiloco_amd.utils.checkpoint import COMPLETE, find_checkpoint
+    d = tmp_path / "ck"
+    assert find_checkpoint(str(d)) is None
+    (tmp_path / "ck.tmp").mkdir()
+    (tmp_path / "ck.tmp" / "trainer_state.json").write_text("{}")
+    assert find_checkpoint(str(d)) is None  # staging only: nothing complete yet
+    (tmp_path / "ck.old").mkdir()
+    (tmp_path / "ck.old" / COMPLETE).write_text('{"step": 4}')
+    assert find_checkpoint(str(d)) == str(tmp_path / "ck.old")  # interrupted between the two renames
+    d.mkdir()
+    (d / COMPLETE).write_text('{"step": 6}')
+    assert find_checkpoint(str(d)) == str(d)
+
+
 def _bench_json(stdout: str) -> dict:
     lines = [l for l in stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, stdout[-2000:]
