@@ -84,6 +84,7 @@ class TrainArgs:
     checkpoint_every: int = 0      # in outer steps (0 = only at the end when checkpoint_dir is set)
     stop_at_step: int = 0          # stop early (simulated preemption) after this inner step; 0 = run to total
     resume: Optional[str] = None   # a checkpoint dir, or "auto": the newest complete one in checkpoint_dir (restarts)
+    elastic_resume: bool = False   # resume on a different number of DiLoCo workers (utils/checkpoint.py)
     log_every: int = 1
     log_file: Optional[str] = None
     wandb: str = "auto"
@@ -205,9 +206,11 @@ class Trainer:
                 print(f"[resume auto] {'from ' + resume if resume else 'no checkpoint: fresh start'}", flush=True)
         if resume:
             from .utils.checkpoint import load_checkpoint
-            st = load_checkpoint(resume, self.model, self.diloco, e)
+            st = load_checkpoint(resume, self.model, self.diloco, e, elastic=a.elastic_resume)
             self.start_step = int(st["step"])
             ds = st.get("data_state")
+            if st.get("resized_from") is not None and e.rank == 0:
+                print(f"[elastic resume] {st['resized_from']} -> {e.world_size} workers", flush=True)
             if ds:
                 # a data stream that cannot be restored must fail the resume loudly: silently
                 # restarting it would re-train on the same tokens
@@ -215,7 +218,8 @@ class Trainer:
                     raise RuntimeError(f"checkpoint has data state but data source {self.data_kind!r} "
                                        f"cannot restore it")
                 self.data.load_state_dict(ds)
-            elif hasattr(self.data, "load_state_dict"):
+            elif hasattr(self.data, "load_state_dict") and st.get("resized_from") is None:
+                # (--elastic-resume: a worker the checkpoint did not have starts a fresh stream by design)
                 raise RuntimeError(f"checkpoint {resume} has no data state for rank {e.rank}; "
                                    f"resuming would restart the data stream")
         self.graphed = None

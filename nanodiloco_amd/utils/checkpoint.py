@@ -142,7 +142,12 @@ def save_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, step: int, data_
     barrier(env)
 
 
-def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv) -> Dict[str, Any]:
+def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, elastic: bool = False) -> Dict[str, Any]:
+    """``elastic`` (``--elastic-resume``): the number of DiLoCo workers may differ from the checkpoint's (one GPU
+    per worker, a checkpoint without a pending overlapped outer step).  The shared outer state (theta_sync,
+    outer momentum, schedule) is exact; worker r keeps its own AdamW state and data stream when the
+    checkpoint has rank r, and a NEW worker starts from rank 0's AdamW state with a fresh data stream -- the
+    "average over the survivors" recovery DiLoCo allows."""
     found = find_checkpoint(ckpt_dir)
     if found is None:
         raise FileNotFoundError(f"no complete checkpoint at {ckpt_dir}")
@@ -150,13 +155,23 @@ def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv) -> Dict[str, Any
     with open(os.path.join(ckpt_dir, "trainer_state.json")) as f:
         state = json.load(f)
     store = model.store
+    old_world = int(state.get("world_size", env.world_size))
+    resized = elastic and old_world != env.world_size
+    if resized:
+        if env.inner_dp != 1 or int(state.get("inner_dp", 1)) != 1:
+            raise ValueError("--elastic-resume needs one GPU per worker (--inner-dp 1) in both runs")
+        if state.get("pending_outer"):
+            raise ValueError(f"checkpoint {ckpt_dir} holds a pending overlapped outer step (per-worker state): "
+                             f"--elastic-resume needs a checkpoint without one")
     # topology: every rank restores its OWN AdamW state and (two-level mode) its shard of the outer
     # step, so a resume on a different layout would silently drop workers' state or mis-shard the
-    # outer momentum -- refuse it
+    # outer momentum -- refuse it (unless --elastic-resume, above)
     for key, have in (("world_size", env.world_size), ("inner_dp", env.inner_dp), ("flat_numel", store.numel)):
+        if key == "world_size" and resized:
+            continue
         if key in state and int(state[key]) != int(have):
             raise ValueError(f"checkpoint {ckpt_dir} was written with {key}={state[key]}, this run has {have}: "
-                             f"resume needs the same world size, --inner-dp and model")
+                             f"resume needs the same world size, --inner-dp and model (or --elastic-resume)")
     sd = _load_st(os.path.join(ckpt_dir, "model.safetensors"))
     model.load_state_dict(sd)
     ds = _load_st(os.path.join(ckpt_dir, "diloco_state.safetensors"))
@@ -166,7 +181,10 @@ def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv) -> Dict[str, Any
                             "outer_step_count": state["outer_step_count"]})
     rfile = os.path.join(ckpt_dir, f"rank{env.rank}.safetensors")
     data_state: Dict[str, Any] = {}
-    if not os.path.exists(rfile) and "world_size" in state:
+    own = os.path.exists(rfile)
+    if not own and resized:  # a worker the checkpoint did not have: rank 0's AdamW state, fresh data stream
+        rfile = os.path.join(ckpt_dir, "rank0.safetensors")
+    elif not own and "world_size" in state:
         raise FileNotFoundError(f"{rfile} missing: the checkpoint is incomplete for rank {env.rank}")
     if os.path.exists(rfile):
         per = _load_st(rfile)
@@ -176,15 +194,17 @@ def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv) -> Dict[str, Any
                                          per["outer.drift_base"].to(diloco.delta.device))
         diloco.inner_optimizer.exp_avg.copy_(per["adamw.exp_avg"])
         diloco.inner_optimizer.exp_avg_sq.copy_(per["adamw.exp_avg_sq"])
-        with open(os.path.join(ckpt_dir, f"rank{env.rank}.json")) as f:
+        with open(rfile[:-len(".safetensors")] + ".json") as f:
             scal = json.load(f)
         diloco.inner_optimizer.step_count = int(scal["adamw_step"])
-        for k, v in per.items():
-            if k.startswith("data."):
-                data_state[k[5:]] = v
-        for k, v in scal.items():
-            if k.startswith("data."):
-                data_state[k[5:]] = v
+        if own:
+            for k, v in per.items():
+                if k.startswith("data."):
+                    data_state[k[5:]] = v
+            for k, v in scal.items():
+                if k.startswith("data."):
+                    data_state[k[5:]] = v
     state["data_state"] = data_state
+    state["resized_from"] = old_world if resized else None
     store.sync_shadow()
     return state

@@ -139,6 +139,33 @@ def test_hung_peer_fails_by_collective_timeout(tmp_path):
     assert "time" in out.lower(), out[-4000:]  # gloo: "Timed out ..." on the waiting rank
 
 
+@pytest.mark.slow
+def test_elastic_resume_changes_worker_count(tmp_path):
+    """--elastic-resume: a 2-worker checkpoint resumes on 1 worker (a lost node) and on 3 workers (a new one
+    joins); the shared outer state is loaded exactly and training continues.  Without the flag the world-size
+    change is refused."""
+    ck = tmp_path / "ck"
+    common = BASE + ["--inner-steps", "2", "--data", "synthetic"]
+    _torchrun(2, common + ["--total-steps", "4", "--checkpoint-dir", str(ck)], tmp_path)
+    sync0 = _tensors(ck / "diloco_state.safetensors")["theta_sync"]
+    r = _torchrun_raw(1, common + ["--total-steps", "6", "--resume", str(ck)], tmp_path)
+    assert r.returncode != 0 and "--elastic-resume" in (r.stdout + r.stderr)
+    for n in (1, 3):
+        out = tmp_path / f"out{n}"
+        log = tmp_path / f"l{n}.jsonl"
+        r = _torchrun(n, common + ["--total-steps", "6", "--resume", str(ck), "--elastic-resume", "--log-file",
+                                   str(log), "--checkpoint-dir", str(out)], tmp_path)
+        assert f"[elastic resume] 2 -> {n} workers" in r.stdout + r.stderr
+        rows = _log(log)
+        assert [x["step"] for x in rows] == [5, 6] and all(x["loss"] == x["loss"] for x in rows)
+        st = json.load(open(out / "trainer_state.json"))
+        assert st["world_size"] == n and st["outer_step_count"] == 3
+    # the resumed runs started from the checkpoint's theta_sync (the 1-worker run's weights after one more
+    # outer step differ from it, but by a training step, not by a re-initialisation)
+    w1 = _tensors(tmp_path / "out1" / "diloco_state.safetensors")["theta_sync"]
+    assert ((w1 - sync0).norm() / sync0.norm()).item() < 0.05
+
+
 def test_find_checkpoint_prefers_complete(tmp_path):
     """Crash consistency of the staging scheme: only a directory with COMPLETE.json (or its .old copy while a
     swap was interrupted) is a resume point; a half-written staging directory never is."""
