@@ -67,3 +67,26 @@ def test_trainer_two_workers_share_gpu_overlap_bf16_comm(tmp_path):
     files = set(_os.listdir(ck)) if ck.is_dir() else set()
     found = files | {f for d in files if (ck / d).is_dir() for f in _os.listdir(ck / d)}
     assert "model.safetensors" in found and "config.json" in found, found
+
+
+def test_crash_restart_resume_auto_rccl_one_gpu(tmp_path):
+    """The §5.3 fault drill on the GPU path: a one-rank torchrun job on the nccl (RCCL) backend crashes after inner
+    step 3 (ND_FAULT_INJECT), ``--max-restarts 1`` restarts it, the restart's c10d store is attempt-prefixed
+    (parallel/dist.py) and ``--resume auto`` continues from the step-2 checkpoint to the end."""
+    ck = tmp_path / "ck"
+    log = tmp_path / "m.jsonl"
+    env = dict(os.environ, OMP_NUM_THREADS="4", PYTHONPATH=ROOT, ND_FAULT_INJECT="0:3")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "--max-restarts", "1", "-m", "nanodiloco_amd",
+           "--llama-config-file", "configs/llama_tiny.json", "--batch-size", "8", "--per-device-batch-size", "4",
+           "--seq-length", "128", "--warmup-steps", "2", "--wandb", "off", "--data", "synthetic",
+           "--inner-steps", "2", "--total-steps", "6", "--backend", "nccl", "--force-collectives", "true",
+           "--checkpoint-dir", str(ck),
+           "--checkpoint-every", "1", "--resume", "auto", "--log-file", str(log)]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "[fault inject] rank 0 step 3: crash" in out and "[resume auto] from" in out, out[-4000:]
+    assert json.load(open(ck / "COMPLETE.json"))["step"] == 6
+    steps = [json.loads(l)["step"] for l in open(log)]
+    assert steps[-1] == 6 and 3 in steps  # step 3 ran (again) after the restart
