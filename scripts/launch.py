@@ -7,6 +7,13 @@ prepare_configs :184-242), for MI355X nodes driven by plain torchrun (no Modal /
   python scripts/launch.py small-single-node                      # all local GPUs, bs 128, lr 1e-3, 5000 steps
   python scripts/launch.py large-multi-node --nnodes 2 --node-rank 0 --master-addr 10.0.0.1
   python scripts/launch.py benchmark --nnodes 1                   # 200 steps, JSONL metrics with comm timings
+  python scripts/launch.py main --fault-tolerant --min-nodes 1    # restarts + elastic worker count (below)
+
+Fault tolerance: ``--fault-tolerant`` adds ``--max-restarts`` (default 3) and makes the trainer
+checkpoint every outer step into ``--checkpoint-dir`` and restart with ``--resume auto`` (the newest COMPLETE
+checkpoint).  ``--min-nodes M`` (< ``--nnodes``) switches torchrun to an elastic c10d rendezvous
+(``--nnodes M:N``) and the trainer to ``--elastic-resume``: after a lost node the job continues on the
+surviving DiLoCo workers.  ``--dry-run`` prints the command only.
 
 Every subcommand starts ``torchrun ... -m nanodiloco_amd`` as a child process and exits with its code.
 Extra arguments after ``--`` are forwarded to the trainer.  (The reference's multi-node path passes
@@ -44,18 +51,35 @@ def _gpus() -> int:
         return 1
 
 
+def torchrun_cmd(a, trainer_args):
+    elastic = bool(a.min_nodes) and a.min_nodes < a.nnodes
+    restarts = a.max_restarts if a.max_restarts is not None else (3 if (a.fault_tolerant or elastic) else 0)
+    nnodes = f"{a.min_nodes}:{a.nnodes}" if elastic else str(a.nnodes)
+    cmd = [sys.executable, "-m", "torch.distributed.run", f"--nnodes={nnodes}",
+           f"--nproc-per-node={a.nproc_per_node or _gpus()}", f"--max-restarts={restarts}"]
+    if elastic:  # the worker count may change between restarts: c10d rendezvous, no fixed node rank
+        cmd += ["--rdzv-backend=c10d", f"--rdzv-endpoint={a.master_addr}:{a.master_port}", f"--rdzv-id={a.run_id}"]
+    elif a.nnodes > 1:
+        cmd += [f"--node-rank={a.node_rank}", f"--master-addr={a.master_addr}", f"--master-port={a.master_port}"]
+    else:
+        cmd += ["--master-addr=127.0.0.1", f"--master-port={a.master_port}"]
+    extra = []
+    if a.fault_tolerant or elastic:
+        ck = a.checkpoint_dir or os.path.join(ROOT, "runs", f"{a.cmd}_ckpt")
+        extra = ["--checkpoint-dir", ck, "--checkpoint-every", "1", "--resume", "auto"]
+        if elastic:
+            extra += ["--elastic-resume", "true"]
+    return cmd + ["-m", "nanodiloco_amd"] + trainer_args + extra + a.extra
+
+
 def _torchrun(a, trainer_args):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", f"--nnodes={a.nnodes}",
-           f"--nproc-per-node={a.nproc_per_node or _gpus()}", f"--max-restarts={a.max_restarts}"]
-    if a.nnodes > 1:
-        cmd += [f"--node-rank={a.node_rank}", f"--master-addr={a.master_addr}", f"--master-port={a.master_port}"]
-    else:
-        cmd += ["--master-addr=127.0.0.1", f"--master-port={a.master_port}"]
-    cmd += ["-m", "nanodiloco_amd"] + trainer_args + a.extra
+    cmd = torchrun_cmd(a, trainer_args)
     print("+", " ".join(cmd), flush=True)
+    if a.dry_run:
+        return 0
     return subprocess.call(cmd, cwd=ROOT, env=env)
 
 
@@ -71,7 +95,13 @@ def main():
         p.add_argument("--master-addr", default=os.environ.get("MASTER_ADDR", "127.0.0.1"))
         p.add_argument("--master-port", type=int, default=int(os.environ.get("MASTER_PORT", 29500)))
         p.add_argument("--nproc-per-node", type=int, default=0)
-        p.add_argument("--max-restarts", type=int, default=0)
+        p.add_argument("--max-restarts", type=int, default=None, help="torchrun restarts (default 0; 3 with --fault-tolerant)")
+        p.add_argument("--fault-tolerant", action="store_true",
+                       help="checkpoint every outer step and restart from the newest complete checkpoint")
+        p.add_argument("--min-nodes", type=int, default=0, help="elastic: continue with as few as this many nodes")
+        p.add_argument("--checkpoint-dir", default=None)
+        p.add_argument("--run-id", default="nanodiloco")
+        p.add_argument("--dry-run", action="store_true", help="print the torchrun command only")
         p.add_argument("--llama-config", default=os.path.join(ROOT, "configs", "llama_default.json"))
         p.add_argument("--run-config", default=os.path.join(ROOT, "configs", "wandb_default.json"))
         p.add_argument("--dataset-path", default="/vol/datasets/PrimeIntellect/c4-tiny/en/save_to_disk")

@@ -100,3 +100,26 @@ def test_trainer_asserts_like_reference():
         Trainer(TrainArgs(batch_size=10, per_device_batch_size=3, device="cpu"))
     with pytest.raises(ValueError):
         Trainer(TrainArgs(total_steps=10, inner_steps=3, device="cpu"))
+
+
+def test_launcher_fault_tolerant_and_elastic_commands():
+    """scripts/launch.py: --fault-tolerant adds restarts + per-outer-step checkpoints + --resume auto; --min-nodes
+    switches to an elastic c10d rendezvous (nnodes MIN:MAX) with --elastic-resume."""
+    import argparse
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("launch", os.path.join(ROOT, "scripts", "launch.py"))
+    L = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(L)
+    base = dict(cmd="main", nnodes=2, node_rank=0, master_addr="10.0.0.1", master_port=29500, nproc_per_node=8,
+                max_restarts=None, fault_tolerant=False, min_nodes=0, checkpoint_dir=None, run_id="r", extra=[],
+                dry_run=True)
+    plain = L.torchrun_cmd(argparse.Namespace(**base), [])
+    assert "--max-restarts=0" in plain and "--resume" not in plain and "--node-rank=0" in plain
+    ft = L.torchrun_cmd(argparse.Namespace(**{**base, "fault_tolerant": True, "checkpoint_dir": "/ck"}), [])
+    assert "--max-restarts=3" in ft and ft[ft.index("--resume") + 1] == "auto" and "/ck" in ft
+    el = L.torchrun_cmd(argparse.Namespace(**{**base, "min_nodes": 1}), [])
+    assert "--nnodes=1:2" in el and "--rdzv-backend=c10d" in el and "--elastic-resume" in el
+    assert "--max-restarts=3" in el and "--node-rank=0" not in el
+    from nanodiloco_amd import main as M
+    a = M.parse_args(el[el.index("nanodiloco_amd") + 1:] + ["--device", "cpu"])
+    assert a.elastic_resume is True and a.resume == "auto" and a.checkpoint_every == 1
