@@ -12,9 +12,19 @@
 //     32-lane half reads land in four different quarters of the bank row (conflict-free);
 //   * split-K: when the output has few tiles, K is split over S workgroups writing fp32 slabs that a
 //     streaming kernel sums into C in a fixed order -- deterministic (no float atomics);
-//   * register-staged prefetch of the next 64-deep K tile is issued before the current tile's MFMAs;
 //   * XCD-aware block remap so the workgroups sharing an A row-panel run on one XCD's L2.
-// Tile: 128 x 128 per 256-thread workgroup (2 x 2 waves of 64 x 64, 2 x 2 v_mfma_f32_32x32x16_bf16).
+//
+// Kernels in this file (dispatch: nd_wgrad / nd_wgrad2 / nd_wgrad_f8 at the end):
+//   wgrad_pp_kernel    the default (K % 64 == 0, >= 8 output tiles of 256 x 256): ping-pong pairing of
+//                      csrc/gemm_pp.hip, LDS-DMA staging, counted vmcnt; one or TWO products per launch
+//                      (nd_wgrad2, round 5: e.g. the MLP's down + gate|up gradients fill the chip together)
+//   wgrad_dma_kernel   256 x 256, 4-wave-pair LDS-DMA kernel of round 2: K % 64 != 0 (register-staged tail)
+//                      and the dma0 / dmas A/B variants
+//   wgrad_kernel       128 x 128 per 256-thread workgroup (2 x 2 waves of 64 x 64, 32x32x16 MFMA),
+//                      register-staged prefetch: outputs with < 8 tiles of 256 x 256
+//   wgrad8_pp_kernel   the fp8 form of the ping-pong kernel (e5m2 / e4m3 dY, e4m3 X, 16x16x128 f8f6f4 MFMA)
+// Split count per launch: a fixed rule (~256 workgroups), replaced by a makespan model where it predicts a
+// >= 10 % win (plan() below).
 #include "common.h"
 #include <cstdlib>
 #include <cstring>
