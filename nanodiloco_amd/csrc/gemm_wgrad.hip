@@ -854,6 +854,14 @@ static int splits_for(int tiles, int K, int bk, int target) {
 
 // Variant choice: the 256 x 256 kernel (1 workgroup / CU) when the output has >= 8 such tiles,
 // else the 128 x 128 kernel.  Returns splits * 2 + (large ? 1 : 0) so the caller can size the slab.
+// A/B hook (scripts/wgrad_splits_ab.py): force the split count of single weight gradients (0 = the plan)
+static int g_wgrad_force_s = 0;
+ND_API int nd_wgrad_force_splits(int s) {
+  const int old = g_wgrad_force_s;
+  g_wgrad_force_s = s > 0 ? (s > 16 ? 16 : s) : 0;
+  return old;
+}
+
 static int plan(int M, int N, int K, int* S_out, bool use_cost = true) {
   const int t256 = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2);
   if (t256 >= 8) {
@@ -867,6 +875,7 @@ static int plan(int M, int N, int K, int* S_out, bool use_cost = true) {
       const int Sc = group_splits(t256, K, (int64_t)M * N);
       if (split_cost(t256, K, (int64_t)M * N, Sc) < g_wgrad_plan_thr * split_cost(t256, K, (int64_t)M * N, S)) S = Sc;
     }
+    if (g_wgrad_force_s > 0) S = g_wgrad_force_s;
     *S_out = S;
     return 1;
   }

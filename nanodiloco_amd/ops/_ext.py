@@ -190,6 +190,7 @@ def _declare(L: ctypes.CDLL):
         # weight-gradient GEMM
         "nd_wgrad_splits": [I, I, I],
         "nd_wgrad_f8_splits": [I, I, I],
+        "nd_wgrad_force_splits": [I],
         "nd_wgrad": [P, P, P, P, I, I, I, L64, L64, L64, P],
         "nd_wgrad2_splits": [I, I, I, I, I],
         "nd_wgrad2": [P, P, P, P, I, I, L64, L64, L64, P, P, P, P, I, I, L64, L64, L64, I, P],
