@@ -74,6 +74,8 @@ def parse():
                          "profiles/r4_wgrad_overlap_ab.md); 0 off; 2 unfenced (A/B only)")
     ap.add_argument("--deterministic", action="store_true",
                     help="bitwise-reproducible step (sorted embedding backward, per-row loss sum; A/B)")
+    ap.add_argument("--residual-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="residual stream dtype (fp32: the autocast recipe, default; bf16: Megatron's default)")
     ap.add_argument("--wgrad-group", type=int, default=1, choices=[0, 1],
                     help="the MLP's down and gate|up weight gradients as one grouped own-kernel launch (1, default)")
     ap.add_argument("--wgrad-variant", default=None,
@@ -137,7 +139,8 @@ def main():
         comm_dtype=a.comm_dtype, bucket_mb=a.bucket_mb, overlap_outer=a.overlap_outer, fp8=a.fp8,
         fp8_wgrad=bool(a.fp8_wgrad), fp8_keep_fused=a.fp8_keep_fused, tuned_gemm=not a.no_tuned_gemm and not a.tuned_gemm_file,
         hip_graph="on" if a.hip_graph else "off", wgrad_overlap=bool(a.wgrad_overlap), log_every=0, wandb="off",
-        phase_timing=False, force_collectives=a.backend != "none" and world == 1, deterministic=a.deterministic)
+        phase_timing=False, force_collectives=a.backend != "none" and world == 1, deterministic=a.deterministic,
+        residual_dtype=a.residual_dtype)
     tr = Trainer(targs)
     env, cfg, dl = tr.env, tr.llama_config, tr.diloco
     ops.set_wgrad_overlap(a.wgrad_overlap)  # mode 2 (unfenced A/B) is not a trainer option
@@ -258,6 +261,7 @@ def main():
             "tuned_gemm": enable_tuned_gemms(env.device) if env.device.type == "cuda" and not a.no_tuned_gemm else False,
             "wgrad_overlap": ops.wgrad_overlap_enabled(),
             "wgrad_group": ops.wgrad_group_enabled(),
+            "residual_dtype": a.residual_dtype,
             "deterministic": bool(a.deterministic),
             "proj_gemm": ops.proj_gemm(),
             "fused_epilogues": ops.fused_epilogues(),

@@ -8,6 +8,10 @@
 // emits dx (fp32) and optionally the branch gradient in the compute dtype, and accumulates
 // dw = sum_rows dy * xhat per lane in registers across the rows a wave visits; the 4 waves of a
 // block combine through LDS and write one partial row per block (host reduces <=1024 partials).
+// Residual stream dtype (round 5): fp32 by default; bf16 (`--residual-dtype bf16`, Megatron's default) keeps
+// h_new, the incoming residual gradient and dx in bf16 -- h_new is rounded BEFORE the statistics so the
+// backward's recomputed xhat matches, and dx doubles as the branch gradient (one bf16 store instead of an fp32
+// dx plus a bf16 da): the forward moves 4 instead of 6 bf16-tensor units, the backward 4 instead of 8.
 #include "common.h"
 
 using namespace nd;
@@ -16,7 +20,7 @@ using namespace nd;
 template <int NCH, int XDT, int ADT, int YDT, bool Q = false>
 __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const void* __restrict__ x, const void* __restrict__ a,
                                                           const float* __restrict__ w, void* __restrict__ y,
-                                                          float* __restrict__ h_out, float* __restrict__ rstd_out,
+                                                          void* __restrict__ h_out, float* __restrict__ rstd_out,
                                                           int64_t rows, int cols, float eps, Fp8Out q8) {
   float qmax = 0.f;
   const float qsc = Q ? q8.scale[0] : 1.f;
@@ -37,7 +41,8 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const void* __restrict
           Vec8<(ADT >= 0 ? ADT : 0)>::load(a, base + col, t);
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[c][j] += t[j];
-          Vec8<F32>::store(h_out, base + col, v[c]);
+          if (XDT == BF16) round_bf16x8(v[c]);  // bf16 residual: statistics of the stored h_new
+          Vec8<XDT>::store(h_out, base + col, v[c]);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
@@ -63,12 +68,15 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const void* __restrict
 }
 
 // Q (DADT == BF16 only): fused fp8 side output of the branch gradient da (common.h Fp8Out).
-template <int NCH, int DYDT, int DADT, bool Q = false>
-__global__ void __launch_bounds__(256, (NCH <= 2 ? 4 : 1)) rmsnorm_bwd_kernel(const void* __restrict__ dy, const float* __restrict__ h,
+// HDT: residual dtype of h, dres and dx.  HDT == BF16 with a bf16 branch gradient: da IS dx (host passes the
+// same pointer) and only the da store runs.
+template <int NCH, int DYDT, int DADT, bool Q = false, int HDT = F32>
+__global__ void __launch_bounds__(256, (NCH <= 2 ? 4 : 1)) rmsnorm_bwd_kernel(const void* __restrict__ dy, const void* __restrict__ h,
                                                           const float* __restrict__ w, const float* __restrict__ rstd,
-                                                          const float* __restrict__ dres, float* __restrict__ dx,
-                                                          void* __restrict__ da, float* __restrict__ part,
+                                                          const void* __restrict__ dres, void* dx,
+                                                          void* da, float* __restrict__ part,
                                                           int64_t rows, int cols, Fp8Out q8) {
+  constexpr bool DXA = HDT == BF16 && (Q || DADT == BF16);  // dx aliases da
   float qmax = 0.f;
   const float qsc = Q ? q8.scale[0] : 1.f;
   extern __shared__ __attribute__((aligned(16))) float sdw[];  // [4 waves][cols] weight-gradient partials
@@ -97,7 +105,7 @@ __global__ void __launch_bounds__(256, (NCH <= 2 ? 4 : 1)) rmsnorm_bwd_kernel(co
       if (col < cols) {
         float d[8];
         Vec8<DYDT>::load(dy, base + col, d);
-        Vec8<F32>::load(h, base + col, xh[c]);
+        Vec8<HDT>::load(h, base + col, xh[c]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[c][j] *= rs;
@@ -113,14 +121,14 @@ __global__ void __launch_bounds__(256, (NCH <= 2 ? 4 : 1)) rmsnorm_bwd_kernel(co
       const int col = (c * 64 + lane) * 8;
       if (col < cols) {
         float o[8];
-        if (dres) Vec8<F32>::load(dres, base + col, o);
+        if (dres) Vec8<HDT>::load(dres, base + col, o);
         else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] = 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] += rs * (g[c][j] - xh[c][j] * dot);
-        Vec8<F32>::store(dx, base + col, o);
+        if (!DXA) Vec8<HDT>::store(dx, base + col, o);
         if (Q) put8_bf16_q(da, base + col, o, q8, qsc, qmax);  // DADT == BF16 (launcher)
         else if (DADT >= 0) Vec8<(DADT >= 0 ? DADT : 0)>::store(da, base + col, o);
       }
@@ -142,19 +150,25 @@ __global__ void __launch_bounds__(256, (NCH <= 2 ? 4 : 1)) rmsnorm_bwd_kernel(co
 
 // ------------------------------------------------------------------------------------ launchers
 template <int NCH>
-static int fwd_dispatch(const void* x, int xdt, const void* a, int adt, const float* w, void* y, int ydt, float* h,
+static int fwd_dispatch(const void* x, int xdt, const void* a, int adt, const float* w, void* y, int ydt, void* h,
                         float* rstd, int64_t rows, int cols, float eps, hipStream_t s, const Fp8Out* q8 = nullptr) {
   int64_t blocks = (rows + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   dim3 g((unsigned)blocks), b(256);
   const Fp8Out none{nullptr, nullptr, nullptr, 1, 0};
   if (q8) {  // fused fp8 side output: bf16 y only
-    if (ydt != BF16 || xdt != F32 || (a != nullptr && adt != BF16)) return (int)hipErrorInvalidValue;
-    if (a == nullptr)
+    if (ydt != BF16 || (xdt != F32 && xdt != BF16) || (a != nullptr && adt != BF16)) return (int)hipErrorInvalidValue;
+    if (a == nullptr && xdt == F32)
       hipLaunchKernelGGL((rmsnorm_fwd_kernel<NCH, F32, -1, BF16, true>), g, b, 0, s, x, a, w, y, h, rstd, rows, cols,
                          eps, *q8);
-    else
+    else if (a == nullptr)
+      hipLaunchKernelGGL((rmsnorm_fwd_kernel<NCH, BF16, -1, BF16, true>), g, b, 0, s, x, a, w, y, h, rstd, rows, cols,
+                         eps, *q8);
+    else if (xdt == F32)
       hipLaunchKernelGGL((rmsnorm_fwd_kernel<NCH, F32, BF16, BF16, true>), g, b, 0, s, x, a, w, y, h, rstd, rows, cols,
+                         eps, *q8);
+    else
+      hipLaunchKernelGGL((rmsnorm_fwd_kernel<NCH, BF16, BF16, BF16, true>), g, b, 0, s, x, a, w, y, h, rstd, rows, cols,
                          eps, *q8);
     ND_LAUNCH_CHECK();
   }
@@ -168,13 +182,14 @@ static int fwd_dispatch(const void* x, int xdt, const void* a, int adt, const fl
     if (xdt == F32 && adt == BF16 && ydt == BF16) ND_RF(F32, BF16, BF16);
     else if (xdt == F32 && adt == F32 && ydt == F32) ND_RF(F32, F32, F32);
     else if (xdt == F32 && adt == F32 && ydt == BF16) ND_RF(F32, F32, BF16);
+    else if (xdt == BF16 && adt == BF16 && ydt == BF16) ND_RF(BF16, BF16, BF16);
     else return (int)hipErrorInvalidValue;
   }
 #undef ND_RF
   ND_LAUNCH_CHECK();
 }
 
-ND_API int nd_rmsnorm_fwd(const void* x, int xdt, const void* a, int adt, const float* w, void* y, int ydt, float* h,
+ND_API int nd_rmsnorm_fwd(const void* x, int xdt, const void* a, int adt, const float* w, void* y, int ydt, void* h,
                           float* rstd, int64_t rows, int cols, float eps, hipStream_t s) {
   if (cols % 8 || cols > 8 * 512) return (int)hipErrorInvalidValue;
   const int nch = (cols + 511) / 512;
@@ -187,8 +202,8 @@ ND_API int nd_rmsnorm_fwd(const void* x, int xdt, const void* a, int adt, const 
 }
 
 template <int NCH>
-static int bwd_dispatch(const void* dy, int dydt, const float* h, const float* w, const float* rstd, const float* dres,
-                        float* dx, int dadt, void* da, int64_t rows, int cols, float* part, hipStream_t s,
+static int bwd_dispatch(const void* dy, int dydt, const void* h, int hdt, const float* w, const float* rstd,
+                        const void* dres, void* dx, int dadt, void* da, int64_t rows, int cols, float* part, hipStream_t s,
                         const Fp8Out* q8 = nullptr) {
   int64_t blocks = (rows + 63) / 64;
   if (blocks > 1024) blocks = 1024;
@@ -197,10 +212,27 @@ static int bwd_dispatch(const void* dy, int dydt, const float* h, const float* w
   const Fp8Out none{nullptr, nullptr, nullptr, 1, 0};
   if (q8) {  // fused fp8 side output: bf16 dy and da only
     if (dydt != BF16 || dadt != BF16 || da == nullptr) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((rmsnorm_bwd_kernel<NCH, BF16, BF16, true>), g, b, lds, s, dy, h, w, rstd, dres, dx, da, part,
-                       rows, cols, *q8);
+    if (hdt == F32)
+      hipLaunchKernelGGL((rmsnorm_bwd_kernel<NCH, BF16, BF16, true>), g, b, lds, s, dy, h, w, rstd, dres, dx, da, part,
+                         rows, cols, *q8);
+    else if (hdt == BF16 && da == dx)
+      hipLaunchKernelGGL((rmsnorm_bwd_kernel<NCH, BF16, BF16, true, BF16>), g, b, lds, s, dy, h, w, rstd, dres, dx, da,
+                         part, rows, cols, *q8);
+    else
+      return (int)hipErrorInvalidValue;
     ND_LAUNCH_CHECK();
   }
+  if (hdt == BF16) {  // bf16 residual: bf16 dy; the branch gradient (if any) is dx itself
+    if (dydt != BF16 || (da != nullptr && (dadt != BF16 || da != dx))) return (int)hipErrorInvalidValue;
+    if (da == nullptr)
+      hipLaunchKernelGGL((rmsnorm_bwd_kernel<NCH, BF16, -1, false, BF16>), g, b, lds, s, dy, h, w, rstd, dres, dx, da,
+                         part, rows, cols, none);
+    else
+      hipLaunchKernelGGL((rmsnorm_bwd_kernel<NCH, BF16, BF16, false, BF16>), g, b, lds, s, dy, h, w, rstd, dres, dx, da,
+                         part, rows, cols, none);
+    ND_LAUNCH_CHECK();
+  }
+  if (hdt != F32) return (int)hipErrorInvalidValue;
 #define ND_RB(D, A) hipLaunchKernelGGL((rmsnorm_bwd_kernel<NCH, D, A>), g, b, lds, s, dy, h, w, rstd, dres, dx, da, part, rows, cols, none)
   if (da == nullptr) {
     if (dydt == BF16) ND_RB(BF16, -1); else ND_RB(F32, -1);
@@ -215,21 +247,22 @@ static int bwd_dispatch(const void* dy, int dydt, const float* h, const float* w
 }
 
 // part must hold min(1024, ceil(rows/64)) * cols floats (the Python side allocates exactly that).
-ND_API int nd_rmsnorm_bwd(const void* dy, int dydt, const float* h, const float* w, const float* rstd,
-                          const float* dres, float* dx, int dadt, void* da, int64_t rows, int cols, float* part,
+// hdt: dtype of h, dres and dx (F32, or BF16 with da == dx or da == nullptr)
+ND_API int nd_rmsnorm_bwd(const void* dy, int dydt, const void* h, int hdt, const float* w, const float* rstd,
+                          const void* dres, void* dx, int dadt, void* da, int64_t rows, int cols, float* part,
                           hipStream_t s) {
   if (cols % 8 || cols > 8 * 512) return (int)hipErrorInvalidValue;
   const int nch = (cols + 511) / 512;
   switch (nch) {
-    case 1: return bwd_dispatch<1>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
-    case 2: return bwd_dispatch<2>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
-    case 3: case 4: return bwd_dispatch<4>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
-    default: return bwd_dispatch<8>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
+    case 1: return bwd_dispatch<1>(dy, dydt, h, hdt, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
+    case 2: return bwd_dispatch<2>(dy, dydt, h, hdt, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
+    case 3: case 4: return bwd_dispatch<4>(dy, dydt, h, hdt, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
+    default: return bwd_dispatch<8>(dy, dydt, h, hdt, w, rstd, dres, dx, dadt, da, rows, cols, part, s);
   }
 }
 
 // fp8 inner step: the same launchers with the fused fp8 side output (q: fp8 bytes shaped like y / da).
-ND_API int nd_rmsnorm_fwd_q(const void* x, int xdt, const void* a, int adt, const float* w, void* y, int ydt, float* h,
+ND_API int nd_rmsnorm_fwd_q(const void* x, int xdt, const void* a, int adt, const float* w, void* y, int ydt, void* h,
                             float* rstd, int64_t rows, int cols, float eps, void* q, const float* scale, float* amax,
                             int parts, int fmt, hipStream_t s) {
   if (cols % 8 || cols > 8 * 512 || !q || !scale || !amax || parts < 1) return (int)hipErrorInvalidValue;
@@ -242,16 +275,16 @@ ND_API int nd_rmsnorm_fwd_q(const void* x, int xdt, const void* a, int adt, cons
   }
 }
 
-ND_API int nd_rmsnorm_bwd_q(const void* dy, int dydt, const float* h, const float* w, const float* rstd,
-                            const float* dres, float* dx, int dadt, void* da, int64_t rows, int cols, float* part,
+ND_API int nd_rmsnorm_bwd_q(const void* dy, int dydt, const void* h, int hdt, const float* w, const float* rstd,
+                            const void* dres, void* dx, int dadt, void* da, int64_t rows, int cols, float* part,
                             void* q, const float* scale, float* amax, int parts, int fmt, hipStream_t s) {
   if (cols % 8 || cols > 8 * 512 || !q || !scale || !amax || parts < 1) return (int)hipErrorInvalidValue;
   const Fp8Out q8{(uint8_t*)q, scale, amax, parts, fmt};
   switch ((cols + 511) / 512) {
-    case 1: return bwd_dispatch<1>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
-    case 2: return bwd_dispatch<2>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
-    case 3: case 4: return bwd_dispatch<4>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
-    default: return bwd_dispatch<8>(dy, dydt, h, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
+    case 1: return bwd_dispatch<1>(dy, dydt, h, hdt, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
+    case 2: return bwd_dispatch<2>(dy, dydt, h, hdt, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
+    case 3: case 4: return bwd_dispatch<4>(dy, dydt, h, hdt, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
+    default: return bwd_dispatch<8>(dy, dydt, h, hdt, w, rstd, dres, dx, dadt, da, rows, cols, part, s, &q8);
   }
 }
 

@@ -71,10 +71,14 @@ class _GradHook(torch.autograd.Function):
 class LlamaForCausalLM:
     def __init__(self, config: LlamaConfig, device="cpu", compute_dtype: torch.dtype = torch.float32,
                  store: Optional[ParamStore] = None, activation_checkpointing: bool = False, fp8: bool = False,
-                 fp8_wgrad: bool = False):
+                 fp8_wgrad: bool = False, residual_dtype: Optional[torch.dtype] = None):
         self.config = config
         self.device = torch.device(device)
         self.compute_dtype = compute_dtype
+        # residual stream: fp32 (default, the autocast recipe) or bf16 (Megatron's default; ops/norm.py)
+        self.residual_dtype = residual_dtype or torch.float32
+        if self.residual_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("residual_dtype must be float32 or bfloat16")
         self.activation_checkpointing = activation_checkpointing
         L = config.num_hidden_layers
         groups = []
@@ -265,6 +269,8 @@ class LlamaForCausalLM:
         eps = c.rms_norm_eps
         cos, sin = ops.rope_cache(T, c.head_dim, c.rope_theta, c.rope_scaling, self.device)
         h = ops.embedding(input_ids, self._m("model.embed_tokens.weight"), self._g("model.embed_tokens.weight"))
+        if self.residual_dtype != h.dtype:
+            h = h.to(self.residual_dtype)
         hook = self.layer_hook if (self.layer_hook is not None and self.training and torch.is_grad_enabled()) else None
         if hook is not None:
             # layer 0's last gradient (its input_layernorm weight) is written by the backward of the

@@ -132,10 +132,10 @@ def _declare(L: ctypes.CDLL):
         "nd_version": [],
         # norms
         "nd_rmsnorm_fwd": [P, I, P, I, P, P, I, P, P, L64, I, F, P],
-        "nd_rmsnorm_bwd": [P, I, P, P, P, P, P, I, P, L64, I, P, P],
+        "nd_rmsnorm_bwd": [P, I, P, I, P, P, P, P, I, P, L64, I, P, P],
         "nd_colsum_add": [P, P, I, I, P],
         "nd_rmsnorm_fwd_q": [P, I, P, I, P, P, I, P, P, L64, I, F, P, P, P, I, I, P],
-        "nd_rmsnorm_bwd_q": [P, I, P, P, P, P, P, I, P, L64, I, P, P, P, P, I, I, P],
+        "nd_rmsnorm_bwd_q": [P, I, P, I, P, P, P, P, I, P, L64, I, P, P, P, P, I, I, P],
         "nd_transpose_bf16": [P, P, I, I, L64, L64, P],
         # rope (in place on packed qkv)
         "nd_rope_inplace": [P, I, P, P, L64, I, I, I, I, I, I, P],

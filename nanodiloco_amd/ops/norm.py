@@ -1,8 +1,10 @@
 """RMSNorm and residual-add + RMSNorm with gradient routing.
 
-Residual stream is kept in fp32 (what HF bf16-autocast effectively does: the embedding output is
+Residual stream is kept in fp32 by default (what HF bf16-autocast effectively does: the embedding output is
 fp32 and every residual add promotes), norm weights are read from the fp32 master, the
-normalised output is emitted in the compute dtype for the next GEMM.
+normalised output is emitted in the compute dtype for the next GEMM.  A bf16 residual stream
+(``--residual-dtype bf16``) is the same ops on a bf16 ``h``: h_new is rounded to bf16 before the
+statistics, the residual gradient is bf16 and doubles as the branch gradient (docs/DESIGN.md, norm passes).
 
 Forward, HIP path: one kernel, one row per wave (``nd_rmsnorm_fwd``) fusing
 ``h_new = h + a`` (K8) with ``y = w * h_new * rstd`` (K2) and saving ``rstd``.
@@ -23,7 +25,7 @@ def _rows(x):
 
 
 def _q8_ok(q8, x, a, out_dtype):
-    return (q8 is not None and out_dtype == torch.bfloat16 and x.dtype == torch.float32
+    return (q8 is not None and out_dtype == torch.bfloat16 and x.dtype in (torch.float32, torch.bfloat16)
             and (a is None or a.dtype == torch.bfloat16))
 
 
@@ -33,7 +35,7 @@ def _hip_fwd(x, a, w, eps, out_dtype, q8=None):
     rows, cols = x2.shape
     y = torch.empty(rows, cols, dtype=out_dtype, device=x.device)
     rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
-    h = torch.empty(rows, cols, dtype=torch.float32, device=x.device) if a is not None else None
+    h = torch.empty(rows, cols, dtype=x.dtype, device=x.device) if a is not None else None
     L = _ext.lib()
     common = (_ext.ptr(x2), _ext.dtcode(x2), _ext.ptr(a), _ext.dtcode(a) if a is not None else 0,
               _ext.ptr(w), _ext.ptr(y), _ext.dtcode(y), _ext.ptr(h), _ext.ptr(rstd), rows, cols, float(eps))
@@ -50,13 +52,18 @@ def _hip_bwd(dy, hx, w, rstd, dres, gw, branch_dtype, q8_bwd=None):
     """``q8_bwd`` (ops/fp8.QuantTarget): also write the fp8 copy of the branch gradient (stashed for
     the projection whose output it is the gradient of)."""
     rows, cols = hx.shape
-    dx = torch.empty(rows, cols, dtype=torch.float32, device=hx.device)
-    da = torch.empty(rows, cols, dtype=branch_dtype, device=hx.device) if branch_dtype is not None else None
+    dx = torch.empty(rows, cols, dtype=hx.dtype, device=hx.device)
+    if branch_dtype is not None and hx.dtype == torch.bfloat16 and branch_dtype == torch.bfloat16:
+        da = dx  # bf16 residual: the residual gradient IS the branch gradient (one store)
+    else:
+        da = torch.empty(rows, cols, dtype=branch_dtype, device=hx.device) if branch_dtype is not None else None
     nblk = min(1024, (rows + 63) // 64)
     part = torch.empty(nblk, cols, dtype=torch.float32, device=hx.device)
     L = _ext.lib()
     dy2 = _rows(dy).contiguous()
-    common = (_ext.ptr(dy2), _ext.dtcode(dy2), _ext.ptr(hx), _ext.ptr(w), _ext.ptr(rstd),
+    if dres is not None and dres.dtype != hx.dtype:
+        dres = dres.to(hx.dtype)
+    common = (_ext.ptr(dy2), _ext.dtcode(dy2), _ext.ptr(hx), _ext.dtcode(hx), _ext.ptr(w), _ext.ptr(rstd),
               _ext.ptr(dres), _ext.ptr(dx), _ext.dtcode(da) if da is not None else 0,
               _ext.ptr(da), rows, cols, _ext.ptr(part))
     if q8_bwd is not None and da is not None and da.dtype == torch.bfloat16 and dy2.dtype == torch.bfloat16:
@@ -124,7 +131,7 @@ class RMSNormResFn(torch.autograd.Function):
             dy = torch.zeros(ctx.shape, dtype=ctx.y_dtype, device=ctx.saved_tensors[0].device)
         if ctx.hip:
             hx, w, rstd = ctx.saved_tensors
-            dr = _rows(dres).float().contiguous() if dres is not None else None
+            dr = _rows(dres).to(hx.dtype).contiguous() if dres is not None else None
             dx, _ = _hip_bwd(dy, hx, w, rstd, dr, ctx.gw, None)
             return dx.view(ctx.shape), None, None, None, None, None
         x, w = ctx.saved_tensors
@@ -144,7 +151,7 @@ class AddRMSNormFn(torch.autograd.Function):
         # the final norm's h_new output is unused: keep its gradient None instead of a zero-filled
         # [N, d] fp32 tensor (a fill plus a full extra read in the backward kernel)
         ctx.set_materialize_grads(False)
-        ctx.eps, ctx.gw, ctx.shape, ctx.a_dtype, ctx.y_dtype = eps, gw, h.shape, a.dtype, out_dtype
+        ctx.eps, ctx.gw, ctx.shape, ctx.a_dtype, ctx.y_dtype, ctx.h_dtype = eps, gw, h.shape, a.dtype, out_dtype, h.dtype
         if _ext.use_hip(h):
             y, hn, rstd = _hip_fwd(h, _rows(a).contiguous(), w, eps, out_dtype, q8)
             ctx.save_for_backward(hn, w, rstd)
@@ -153,6 +160,8 @@ class AddRMSNormFn(torch.autograd.Function):
             return y.view(h.shape), hn.view(h.shape)
         ctx.hip = False
         hn = h.float() + a.float()
+        if h.dtype != torch.float32:  # bf16 residual: statistics of the stored (rounded) h_new
+            hn = hn.to(h.dtype).float()
         ctx.save_for_backward(hn, w)
         return ref.rmsnorm(hn, w, eps).to(out_dtype), hn.to(h.dtype)
 
@@ -171,6 +180,8 @@ class AddRMSNormFn(torch.autograd.Function):
             dx = dx + dhn.float()
         if ctx.gw is not None:
             ctx.gw.add_(dw)
+        if ctx.h_dtype != torch.float32:
+            dx = dx.to(ctx.h_dtype)
         return dx, dx.to(ctx.a_dtype), None, None, None, None, None, None
 
 

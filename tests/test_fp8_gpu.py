@@ -189,11 +189,13 @@ def test_fused_swiglu_quant_bitwise(fmt):
     assert rb.amax[kb].max().item() == dgu.float().abs().max().item()
 
 
+@pytest.mark.parametrize("hdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("residual", [False, True])
-def test_fused_rmsnorm_quant_bitwise(residual):
-    """RMSNorm fwd (y -> e4m3) and bwd (branch grad -> e5m2) fp8 side outputs == separate casts."""
+def test_fused_rmsnorm_quant_bitwise(residual, hdt):
+    """RMSNorm fwd (y -> e4m3) and bwd (branch grad -> e5m2) fp8 side outputs == separate casts (fp32 and bf16
+    residual streams)."""
     rows, cols = 777, 1024
-    h = torch.randn(rows, cols, device="cuda")
+    h = torch.randn(rows, cols, device="cuda").to(hdt)
     a = torch.randn(rows, cols, device="cuda").bfloat16()
     w = 1 + 0.1 * torch.randn(cols, device="cuda")
     r, k, q = _target(fp8.E4M3, 50.0)

@@ -81,6 +81,62 @@ def test_rmsnorm_res_fused_residual_grad():
     assert rel(gw, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("cols", [1024, 2048])
+def test_add_rmsnorm_bf16_residual(cols):
+    """bf16 residual stream (--residual-dtype bf16): h_new is the RNE-rounded h + a (bitwise), y / dh / da /
+    dw match an fp32 reference computed from that rounded h_new, and the residual gradient IS the branch
+    gradient (one bf16 tensor)."""
+    rows, eps = 1000, 1e-5
+    h = torch.randn(rows, cols, device=DEV).bfloat16()
+    a = torch.randn(rows, cols, device=DEV).bfloat16()
+    w = 1 + 0.1 * torch.randn(cols, device=DEV)
+    dres = torch.randn(rows, cols, device=DEV).bfloat16()
+    dy = torch.randn(rows, cols, device=DEV).bfloat16()
+    hn_ref = (h.float() + a.float()).bfloat16()
+    xr = hn_ref.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = wr * (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + eps))
+    ((yr * dy.float()).sum() + (xr * dres.float()).sum()).backward()
+    hx, ax = h.clone().requires_grad_(True), a.clone().requires_grad_(True)
+    gw = torch.zeros(cols, device=DEV)
+    y, hn = ops.add_rmsnorm(hx, ax, w, gw, eps, torch.bfloat16)
+    assert hn.dtype == torch.bfloat16 and torch.equal(hn, hn_ref)
+    assert rel(y, yr) < 5e-3
+    dh, da = torch.autograd.grad((y, hn), (hx, ax), (dy, dres))
+    assert dh.dtype == torch.bfloat16 and da.dtype == torch.bfloat16
+    assert dh.data_ptr() == da.data_ptr()  # one store serves both
+    assert rel(dh, xr.grad) < 1e-2
+    gw2 = torch.zeros(cols, device=DEV)
+    hx2, ax2 = h.clone().requires_grad_(True), a.clone().requires_grad_(True)
+    y2, _ = ops.add_rmsnorm(hx2, ax2, w, gw2, eps, torch.bfloat16)
+    (y2.float() * dy.float()).sum().backward()
+    wr2 = w.clone().requires_grad_(True)
+    x2 = hn_ref.float()
+    (wr2 * (x2 * torch.rsqrt(x2.pow(2).mean(-1, keepdim=True) + eps)) * dy.float()).sum().backward()
+    assert rel(gw2, wr2.grad) < 1e-2
+
+
+def test_rmsnorm_res_bf16_residual():
+    """First norm on a bf16 residual stream: bf16 dres in, bf16 dx out, fp32 reference."""
+    rows, cols, eps = 1000, 1024, 1e-5
+    x = torch.randn(rows, cols, device=DEV).bfloat16()
+    w = 1 + 0.1 * torch.randn(cols, device=DEV)
+    up = torch.randn(rows, cols, device=DEV).bfloat16()
+    ur = torch.randn(rows, cols, device=DEV).bfloat16()
+    xr = x.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = wr * (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + eps))
+    ((yr * up.float()).sum() + (xr * ur.float()).sum()).backward()
+    xx = x.clone().requires_grad_(True)
+    gw = torch.zeros(cols, device=DEV)
+    y, h = ops.rmsnorm_res(xx, w, gw, eps, torch.bfloat16)
+    torch.autograd.backward((y, h), (up, ur))
+    assert xx.grad.dtype == torch.bfloat16
+    assert rel(y, yr) < 5e-3
+    assert rel(xx.grad, xr.grad) < 1e-2
+    assert rel(gw, wr.grad) < 1e-2
+
+
 # ----------------------------------------------------------------------------------- rope
 @pytest.mark.parametrize("hd,nh,nkv", [(64, 4, 4), (128, 4, 2), (32, 4, 1)])
 def test_rope_inplace_matches_reference(hd, nh, nkv, hip_lib):

@@ -109,6 +109,39 @@ def test_rmsnorm_res_fuses_residual_grad():
     torch.testing.assert_close(xx.grad, xr.grad)
 
 
+def test_bf16_residual_stream_tracks_fp32():
+    """--residual-dtype bf16 on the PyTorch path: the residual stream and its gradient are bf16 tensors, and loss /
+    gradients stay within bf16 rounding of the fp32-residual model (same weights, same batch)."""
+    c = LlamaConfig.from_dict(dict(hidden_size=64, intermediate_size=128, num_attention_heads=4,
+                                   num_key_value_heads=2, num_hidden_layers=2, vocab_size=97))
+    ids = torch.randint(0, 97, (3, 24), generator=torch.Generator().manual_seed(0))
+    res = {}
+    for rdt in (None, torch.bfloat16):
+        m = LlamaForCausalLM(c, residual_dtype=rdt).init_weights(1)
+        loss = m(ids, labels=ids).loss
+        loss.backward()
+        res[rdt] = (loss.item(), m.store.grad.clone())
+    (l32, g32), (l16, g16) = res[None], res[torch.bfloat16]
+    assert abs(l32 - l16) < 1e-2 * l32
+    assert ((g32 - g16).norm() / g32.norm()).item() < 3e-2
+    with pytest.raises(ValueError):
+        LlamaForCausalLM(c, residual_dtype=torch.float16)
+
+
+def test_bf16_residual_add_rmsnorm_rounds_h_new():
+    """The PyTorch fallback of add_rmsnorm on a bf16 residual: h_new is the RNE-rounded sum and the norm's
+    statistics are those of the rounded value (what the HIP kernel stores and the backward recomputes from)."""
+    from nanodiloco_amd import ops
+    torch.manual_seed(0)
+    h = torch.randn(5, 32).bfloat16()
+    a = torch.randn(5, 32).bfloat16()
+    w = torch.randn(32)
+    y, hn = ops.add_rmsnorm(h, a, w, None, 1e-5, torch.float32)
+    assert hn.dtype == torch.bfloat16 and torch.equal(hn, (h.float() + a.float()).bfloat16())
+    x = hn.float()
+    torch.testing.assert_close(y, w * (x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-5)))
+
+
 @pytest.mark.parametrize("side", ["left", "right"])
 def test_padded_batch_matches_hf_attention_mask(side):
     """Padded batches (the reference's tokenizer.pad + attention_mask, REF/nanodiloco/main.py:79-88,109):

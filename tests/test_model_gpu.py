@@ -18,9 +18,9 @@ def _gpu(hip_lib):
     ops.set_backend("auto")
 
 
-def _run(cfg, backend, ids, dtype):
+def _run(cfg, backend, ids, dtype, residual_dtype=None, fp8=False):
     ops.set_backend(backend)
-    m = LlamaForCausalLM(cfg, "cuda", dtype).init_weights(3)
+    m = LlamaForCausalLM(cfg, "cuda", dtype, residual_dtype=residual_dtype, fp8=fp8).init_weights(3)
     out = m(ids, labels=ids)
     out.loss.backward()
     torch.cuda.synchronize()
@@ -40,10 +40,26 @@ def test_hip_vs_torch_model(kv):
     assert rel < 5e-2, rel
 
 
-def test_hip_vs_torch_loss_trajectory():
+@pytest.mark.parametrize("fp8", [False, True])
+def test_bf16_residual_model_tracks_fp32(fp8):
+    """--residual-dtype bf16 (HIP, bf16 compute, optionally fp8 projections) against the fp32 torch model:
+    the same tolerances as the fp32-residual HIP model."""
+    cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                                     num_key_value_heads=2, num_hidden_layers=2, vocab_size=1000,
+                                     rms_norm_eps=1e-5))
+    ids = torch.randint(0, 1000, (2, 256), device="cuda")
+    l_t, g_t = _run(cfg, "torch", ids, torch.float32)
+    l_h, g_h = _run(cfg, "hip", ids, torch.bfloat16, residual_dtype=torch.bfloat16, fp8=fp8)
+    assert abs(l_t - l_h) < 2e-2 * abs(l_t)
+    rel = ((g_t - g_h).norm() / g_t.norm()).item()
+    assert rel < (1e-1 if fp8 else 5e-2), rel
+
+
+@pytest.mark.parametrize("res", ["fp32", "bf16"])
+def test_hip_vs_torch_loss_trajectory(res):
     """40 clip + AdamW steps on learnable data (every sequence follows one fixed random next-token
     permutation): the HIP bf16 model tracks the fp32 torch model's loss curve step by step, on fresh
-    batches (not a memorised one), GQA 4/2."""
+    batches (not a memorised one), GQA 4/2; with the fp32 and the bf16 residual stream."""
     V = 512
     cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=512, num_attention_heads=4,
                                      num_key_value_heads=2, num_hidden_layers=2, vocab_size=V,
@@ -60,7 +76,8 @@ def test_hip_vs_torch_loss_trajectory():
     curves = {}
     for backend, dt in (("torch", torch.float32), ("hip", torch.bfloat16)):
         ops.set_backend(backend)
-        m = LlamaForCausalLM(cfg, "cuda", dt).init_weights(3)
+        rdt = torch.bfloat16 if (backend == "hip" and res == "bf16") else None
+        m = LlamaForCausalLM(cfg, "cuda", dt, residual_dtype=rdt).init_weights(3)
         opt = FlatAdamW(m.store, lr=1.5e-3)
         ls = []
         for step in range(40):
