@@ -74,8 +74,9 @@ def parse():
                          "profiles/r4_wgrad_overlap_ab.md); 0 off; 2 unfenced (A/B only)")
     ap.add_argument("--deterministic", action="store_true",
                     help="bitwise-reproducible step (sorted embedding backward, per-row loss sum; A/B)")
-    ap.add_argument("--residual-dtype", default="fp32", choices=["fp32", "bf16"],
-                    help="residual stream dtype (fp32: the autocast recipe, default; bf16: Megatron's default)")
+    ap.add_argument("--residual-dtype", default="auto", choices=["auto", "fp32", "bf16"],
+                    help="residual stream dtype (fp32: the autocast recipe; bf16: Megatron's default; "
+                         "auto, the default: bf16 with --fp8, else fp32)")
     ap.add_argument("--wgrad-group", type=int, default=1, choices=[0, 1],
                     help="the MLP's down and gate|up weight gradients as one grouped own-kernel launch (1, default)")
     ap.add_argument("--wgrad-variant", default=None,
@@ -261,7 +262,7 @@ def main():
             "tuned_gemm": enable_tuned_gemms(env.device) if env.device.type == "cuda" and not a.no_tuned_gemm else False,
             "wgrad_overlap": ops.wgrad_overlap_enabled(),
             "wgrad_group": ops.wgrad_group_enabled(),
-            "residual_dtype": a.residual_dtype,
+            "residual_dtype": "bf16" if tr.model.residual_dtype == torch.bfloat16 else "fp32",
             "deterministic": bool(a.deterministic),
             "proj_gemm": ops.proj_gemm(),
             "fused_epilogues": ops.fused_epilogues(),

@@ -66,8 +66,9 @@ class TrainArgs:
     offload_snapshot: bool = False
     legacy_grad_sum: bool = False
     activation_checkpointing: bool = False
-    residual_dtype: str = "fp32"   # fp32 (the autocast recipe) | bf16: residual stream in bf16 (Megatron's default;
-                                   # the RMSNorm passes move 4 instead of 6 / 8 tensor units, docs/DESIGN.md)
+    residual_dtype: str = "auto"   # fp32 (the autocast recipe) | bf16: residual stream in bf16 (Megatron's default;
+                                   # the RMSNorm passes move 4 instead of 6 / 8 tensor units, docs/DESIGN.md) |
+                                   # auto: bf16 with --fp8 (the Megatron / Transformer-Engine fp8 recipe), else fp32
     fp8: bool = False              # fp8 e4m3/e5m2 decoder projections (GPU, bf16 compute)
     fp8_wgrad: bool = True         # with fp8: the weight-gradient GEMMs in fp8 too (own kernel on the token-major
                                    # fp8 operands, 1.65-1.73x the bf16 one; profiles/r4_fp8_pp.md)
@@ -108,10 +109,12 @@ def _dtype(name: str, device: torch.device) -> torch.dtype:
             "bfloat16": torch.bfloat16, "fp8": torch.bfloat16}[name]
 
 
-def _residual_dtype(name: str) -> torch.dtype:
+def _residual_dtype(name: str, fp8: bool = False) -> torch.dtype:
+    if name == "auto":
+        return torch.bfloat16 if fp8 else torch.float32
     d = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}.get(name)
     if d is None:
-        raise ValueError(f"--residual-dtype must be fp32 or bf16, not {name!r}")
+        raise ValueError(f"--residual-dtype must be auto, fp32 or bf16, not {name!r}")
     return d
 
 
@@ -192,7 +195,7 @@ class Trainer:
         self.model = LlamaForCausalLM(self.llama_config, e.device, self.compute_dtype,
                                       activation_checkpointing=a.activation_checkpointing,
                                       fp8=a.fp8 or a.dtype == "fp8", fp8_wgrad=a.fp8_wgrad,
-                                      residual_dtype=_residual_dtype(a.residual_dtype)).init_weights(a.seed)
+                                      residual_dtype=_residual_dtype(a.residual_dtype, a.fp8 or a.dtype == "fp8")).init_weights(a.seed)
         inner = FlatAdamW(self.model.store, lr=a.lr, weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm,
                           skip_nonfinite=a.skip_nonfinite)
         outer = FlatOuterNesterov(self.model.store, lr=a.outer_lr, momentum=a.outer_momentum)

@@ -123,3 +123,16 @@ def test_launcher_fault_tolerant_and_elastic_commands():
     from nanodiloco_amd import main as M
     a = M.parse_args(el[el.index("nanodiloco_amd") + 1:] + ["--device", "cpu"])
     assert a.elastic_resume is True and a.resume == "auto" and a.checkpoint_every == 1
+
+
+def test_residual_dtype_auto():
+    """--residual-dtype auto: bf16 with --fp8 (the Megatron / TE fp8 recipe), fp32 otherwise."""
+    import torch
+
+    from nanodiloco_amd.trainer import _residual_dtype
+    assert _residual_dtype("auto") == torch.float32
+    assert _residual_dtype("auto", fp8=True) == torch.bfloat16
+    assert _residual_dtype("fp32", fp8=True) == torch.float32
+    assert _residual_dtype("bf16") == torch.bfloat16
+    with pytest.raises(ValueError):
+        _residual_dtype("fp16")
