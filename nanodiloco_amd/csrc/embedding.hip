@@ -1,5 +1,6 @@
 // Token embedding gather / scatter-add (K1) on fp32 tables.
-//   fwd: out[i, :] = W[ids[i], :]        one wave per row, 16-B loads/stores
+//   fwd: out[i, :] = W[ids[i], :]        one wave per row, 16-B loads/stores; out fp32, or bf16 (RNE) for the
+//                                        bf16 residual stream (then dy of the backward is bf16 too)
 //   bwd: gW[ids[i], :] += dy[i, :]       one wave per row, each wave-instruction = 64 f32 atomics on
 //                                        256 contiguous bytes (full-rate atomic shape on MI355X)
 // Out-of-range ids are skipped (fwd writes zeros) instead of faulting the device.
@@ -7,8 +8,21 @@
 
 using namespace nd;
 
+__device__ __forceinline__ void put4(float* out, int64_t i, float4 v) { *reinterpret_cast<float4*>(out + i) = v; }
+__device__ __forceinline__ void put4(bf16_t* out, int64_t i, float4 v) {
+  *reinterpret_cast<uint2*>(out + i) = make_uint2(pack2(v.x, v.y), pack2(v.z, v.w));
+}
+__device__ __forceinline__ float4 get4(const float* p, int64_t i) { return *reinterpret_cast<const float4*>(p + i); }
+__device__ __forceinline__ float4 get4(const bf16_t* p, int64_t i) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p + i);
+  return make_float4(lo_bf(u.x), hi_bf(u.x), lo_bf(u.y), hi_bf(u.y));
+}
+__device__ __forceinline__ float get1(const float* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float get1(const bf16_t* p, int64_t i) { return bf2f(p[i]); }
+
+template <typename OT>
 __global__ void __launch_bounds__(256) embed_fwd_kernel(const int64_t* __restrict__ ids, const float* __restrict__ W,
-                                                        float* __restrict__ out, int64_t n, int d, int V) {
+                                                        OT* __restrict__ out, int64_t n, int d, int V) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   for (int64_t r = wave; r < n; r += (int64_t)gridDim.x * 4) {
@@ -16,19 +30,20 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(const int64_t* __restric
     const bool ok = id >= 0 && id < V;
     for (int c = lane * 4; c < d; c += 256) {
       float4 v = ok ? *reinterpret_cast<const float4*>(W + id * d + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(out + r * d + c) = v;
+      put4(out, r * d + c, v);
     }
   }
 }
 
-__global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* __restrict__ ids, const float* __restrict__ dy,
+template <typename DT>
+__global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* __restrict__ ids, const DT* __restrict__ dy,
                                                         float* __restrict__ gW, int64_t n, int d, int V) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   for (int64_t r = wave; r < n; r += (int64_t)gridDim.x * 4) {
     const int64_t id = ids[r];
     if (id < 0 || id >= V) continue;
-    for (int c = lane; c < d; c += 64) atomicAdd(gW + id * d + c, dy[r * d + c]);
+    for (int c = lane; c < d; c += 64) atomicAdd(gW + id * d + c, get1(dy, r * d + c));
   }
 }
 
@@ -44,9 +59,10 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* __restric
 //     in chunk order, then one read-add-write of the table row.
 constexpr int kEmbChunk = 64;
 
+template <typename DT>
 __global__ void __launch_bounds__(256) embed_bwd_sorted_chunks_kernel(const int64_t* __restrict__ sid,
                                                                       const int64_t* __restrict__ perm,
-                                                                      const float* __restrict__ dy,
+                                                                      const DT* __restrict__ dy,
                                                                       float* __restrict__ gW, float* __restrict__ head,
                                                                       float* __restrict__ tail, int64_t n, int d, int V) {
   const int lane = threadIdx.x & 63;
@@ -64,7 +80,7 @@ __global__ void __launch_bounds__(256) embed_bwd_sorted_chunks_kernel(const int6
         for (int col = lane * 4; col < d; col += 256) {
           float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
           for (int64_t k = j; k < e; ++k) {
-            const float4 v = *reinterpret_cast<const float4*>(dy + perm[k] * d + col);
+            const float4 v = get4(dy, perm[k] * d + col);
             acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
           }
           float4* g = reinterpret_cast<float4*>(dst + col);
@@ -109,8 +125,9 @@ __global__ void __launch_bounds__(256) embed_bwd_sorted_join_kernel(const int64_
 }
 
 // ws: 2 * ceil(n / 64) * d floats (head and tail partials); no initialisation needed.
-ND_API int nd_embedding_bwd_sorted(const int64_t* sid, const int64_t* perm, const float* dy, float* gW, float* ws,
-                                   int64_t n, int d, int V, hipStream_t s) {
+// ddt: dtype of dy (F32 / BF16)
+ND_API int nd_embedding_bwd_sorted(const int64_t* sid, const int64_t* perm, const void* dy, int ddt, float* gW,
+                                   float* ws, int64_t n, int d, int V, hipStream_t s) {
   if (d % 4) return (int)hipErrorInvalidValue;
   if (n <= 0) return 0;
   const int64_t nchunks = (n + kEmbChunk - 1) / kEmbChunk;
@@ -118,25 +135,47 @@ ND_API int nd_embedding_bwd_sorted(const int64_t* sid, const int64_t* perm, cons
   float* tail = ws + nchunks * d;
   int64_t blocks = (nchunks + 3) / 4;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(embed_bwd_sorted_chunks_kernel, dim3((unsigned)blocks), dim3(256), 0, s, sid, perm, dy, gW, head,
-                     tail, n, d, V);
+  if (ddt == F32)
+    hipLaunchKernelGGL(embed_bwd_sorted_chunks_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, sid, perm,
+                       (const float*)dy, gW, head, tail, n, d, V);
+  else if (ddt == BF16)
+    hipLaunchKernelGGL(embed_bwd_sorted_chunks_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, s, sid, perm,
+                       (const bf16_t*)dy, gW, head, tail, n, d, V);
+  else
+    return (int)hipErrorInvalidValue;
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(embed_bwd_sorted_join_kernel, dim3((unsigned)blocks), dim3(256), 0, s, sid, gW, head, tail, n, d,
                      V);
   ND_LAUNCH_CHECK();
 }
 
-ND_API int nd_embedding_fwd(const int64_t* ids, const float* W, float* out, int64_t n, int d, int V, hipStream_t s) {
+// odt: dtype of out (F32 / BF16)
+ND_API int nd_embedding_fwd(const int64_t* ids, const float* W, void* out, int odt, int64_t n, int d, int V,
+                            hipStream_t s) {
   if (d % 4) return (int)hipErrorInvalidValue;
   int64_t blocks = (n + 3) / 4;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(embed_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ids, W, out, n, d, V);
+  if (odt == F32)
+    hipLaunchKernelGGL(embed_fwd_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, ids, W, (float*)out, n, d, V);
+  else if (odt == BF16)
+    hipLaunchKernelGGL(embed_fwd_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, s, ids, W, (bf16_t*)out, n, d,
+                       V);
+  else
+    return (int)hipErrorInvalidValue;
   ND_LAUNCH_CHECK();
 }
 
-ND_API int nd_embedding_bwd(const int64_t* ids, const float* dy, float* gW, int64_t n, int d, int V, hipStream_t s) {
+ND_API int nd_embedding_bwd(const int64_t* ids, const void* dy, int ddt, float* gW, int64_t n, int d, int V,
+                            hipStream_t s) {
   int64_t blocks = (n + 3) / 4;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ids, dy, gW, n, d, V);
+  if (ddt == F32)
+    hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, ids, (const float*)dy, gW, n,
+                       d, V);
+  else if (ddt == BF16)
+    hipLaunchKernelGGL(embed_bwd_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, s, ids, (const bf16_t*)dy, gW,
+                       n, d, V);
+  else
+    return (int)hipErrorInvalidValue;
   ND_LAUNCH_CHECK();
 }

@@ -268,9 +268,8 @@ class LlamaForCausalLM:
         cdt = self.compute_dtype
         eps = c.rms_norm_eps
         cos, sin = ops.rope_cache(T, c.head_dim, c.rope_theta, c.rope_scaling, self.device)
-        h = ops.embedding(input_ids, self._m("model.embed_tokens.weight"), self._g("model.embed_tokens.weight"))
-        if self.residual_dtype != h.dtype:
-            h = h.to(self.residual_dtype)
+        h = ops.embedding(input_ids, self._m("model.embed_tokens.weight"), self._g("model.embed_tokens.weight"),
+                          out_dtype=self.residual_dtype)
         hook = self.layer_hook if (self.layer_hook is not None and self.training and torch.is_grad_enabled()) else None
         if hook is not None:
             # layer 0's last gradient (its input_layernorm weight) is written by the backward of the

@@ -155,9 +155,9 @@ def _declare(L: ctypes.CDLL):
         # loss
         "nd_ce_fwd_bwd": [P, I, P, P, P, L64, I, I, P, P, F, P],
         # embedding
-        "nd_embedding_fwd": [P, P, P, L64, I, I, P],
-        "nd_embedding_bwd": [P, P, P, L64, I, I, P],
-        "nd_embedding_bwd_sorted": [P, P, P, P, P, L64, I, I, P],
+        "nd_embedding_fwd": [P, P, P, I, L64, I, I, P],
+        "nd_embedding_bwd": [P, P, I, P, L64, I, I, P],
+        "nd_embedding_bwd_sorted": [P, P, P, I, P, P, L64, I, I, P],
         # optimizer / outer step (flat buffers)
         "nd_sumsq_partial": [P, L64, P, I, P],
         "nd_adamw_step": [P, P, P, P, P, I, L64, P, I, F, F, F, F, F, F, F, F, P, I, P, P],

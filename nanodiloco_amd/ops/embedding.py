@@ -1,5 +1,6 @@
-"""Token embedding (K1): gather rows of the fp32 master table into the fp32 residual stream;
-backward scatter-adds the residual gradient rows into the flat fp32 grad buffer.
+"""Token embedding (K1): gather rows of the fp32 master table into the residual stream (fp32, or bf16 for
+``--residual-dtype bf16``: rounded in the gather, no separate cast pass); backward scatter-adds the residual
+gradient rows (fp32 or bf16) into the flat fp32 grad buffer.
 
 HIP path: ``nd_embedding_fwd`` (one wave per token row, 16-B vector loads) and
 ``nd_embedding_bwd`` (one wave per token row, f32 atomics on whole contiguous rows -- the
@@ -18,20 +19,21 @@ from .determinism import deterministic
 
 class EmbeddingFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, w, gw, anchor):
+    def forward(ctx, ids, w, gw, anchor, out_dtype=None):
         ids = ids.reshape(-1)
         ctx.save_for_backward(ids)
         ctx.gw = gw
         ctx.vocab = w.shape[0]
-        if _ext.use_hip(w):
+        odt = out_dtype or w.dtype
+        if _ext.use_hip(w) and w.dtype == torch.float32:
             n, d = ids.numel(), w.shape[1]
-            out = torch.empty(n, d, dtype=w.dtype, device=w.device)
-            _ext.check(_ext.lib().nd_embedding_fwd(_ext.ptr(ids), _ext.ptr(w), _ext.ptr(out), n, d, w.shape[0],
-                                                   _ext.stream_ptr(w.device)), "nd_embedding_fwd")
+            out = torch.empty(n, d, dtype=odt, device=w.device)
+            _ext.check(_ext.lib().nd_embedding_fwd(_ext.ptr(ids), _ext.ptr(w), _ext.ptr(out), _ext.dtcode(out), n, d,
+                                                   w.shape[0], _ext.stream_ptr(w.device)), "nd_embedding_fwd")
             ctx.hip = True
             return out
         ctx.hip = False
-        return w.index_select(0, ids)
+        return w.index_select(0, ids).to(odt)
 
     @staticmethod
     def backward(ctx, dy):
@@ -44,19 +46,20 @@ class EmbeddingFn(torch.autograd.Function):
                     perm = torch.argsort(ids, stable=True)
                     sid = ids.index_select(0, perm).contiguous()
                     ws = sorted_bwd_workspace(n, d, dy.device)
-                    _ext.check(_ext.lib().nd_embedding_bwd_sorted(_ext.ptr(sid), _ext.ptr(perm), _ext.ptr(dy),
-                                                                  _ext.ptr(ctx.gw), _ext.ptr(ws), n, d, ctx.vocab,
-                                                                  _ext.stream_ptr(dy.device)), "nd_embedding_bwd_sorted")
+                    _ext.check(_ext.lib().nd_embedding_bwd_sorted(
+                        _ext.ptr(sid), _ext.ptr(perm), _ext.ptr(dy), _ext.dtcode(dy), _ext.ptr(ctx.gw), _ext.ptr(ws),
+                        n, d, ctx.vocab, _ext.stream_ptr(dy.device)), "nd_embedding_bwd_sorted")
                 else:
-                    _ext.check(_ext.lib().nd_embedding_bwd(_ext.ptr(ids), _ext.ptr(dy), _ext.ptr(ctx.gw), n, d,
-                                                           ctx.vocab, _ext.stream_ptr(dy.device)), "nd_embedding_bwd")
+                    _ext.check(_ext.lib().nd_embedding_bwd(_ext.ptr(ids), _ext.ptr(dy), _ext.dtcode(dy),
+                                                           _ext.ptr(ctx.gw), n, d, ctx.vocab,
+                                                           _ext.stream_ptr(dy.device)), "nd_embedding_bwd")
             else:
                 ctx.gw.index_add_(0, ids, dy.float())
         # the embedding backward is the last op of the model's backward: join the side-stream
         # weight-gradient GEMMs here so the grad buffer is complete on the compute stream
         from .linear import join_wgrad
         join_wgrad(dy.device if dy.is_cuda else None)
-        return None, None, None, None
+        return None, None, None, None, None
 
 
 _ANCHORS = {}
@@ -79,5 +82,6 @@ def _anchor(device):
     return a
 
 
-def embedding(ids, w, gw):
-    return EmbeddingFn.apply(ids, w, gw, _anchor(w.device))
+def embedding(ids, w, gw, out_dtype=None):
+    """``out_dtype``: dtype of the gathered rows (default: the table's)."""
+    return EmbeddingFn.apply(ids, w, gw, _anchor(w.device), out_dtype)

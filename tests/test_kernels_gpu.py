@@ -176,16 +176,18 @@ def test_swiglu(F):
 
 
 # ----------------------------------------------------------------------------------- embedding
-def test_embedding():
+@pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
+def test_embedding(odt):
+    """fp32 rows, or bf16 rows (RNE in the gather) for the bf16 residual stream with a bf16 dy backward."""
     V, d, n = 1000, 256, 4096
     W = torch.randn(V, d, device=DEV)
     gW = torch.zeros(V, d, device=DEV)
     ids = torch.randint(0, V, (4, n // 4), device=DEV)
-    out = ops.embedding(ids, W, gW)
-    assert torch.equal(out, W[ids.reshape(-1)])
-    dy = torch.randn(n, d, device=DEV)
+    out = ops.embedding(ids, W, gW, out_dtype=odt)
+    assert out.dtype == odt and torch.equal(out, W[ids.reshape(-1)].to(odt))
+    dy = torch.randn(n, d, device=DEV).to(odt)
     out.backward(dy)
-    ref_g = torch.zeros(V, d, device=DEV).index_add_(0, ids.reshape(-1), dy)
+    ref_g = torch.zeros(V, d, device=DEV).index_add_(0, ids.reshape(-1), dy.float())
     assert rel(gW, ref_g) < 1e-6
 
 
@@ -555,8 +557,9 @@ def test_model_left_padded_hip_vs_torch():
     assert abs(losses[0] - losses[1]) < 2e-2 * abs(losses[1]), losses
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", ["repeated", "left_pad", "chunk_edges"])
-def test_embedding_sorted_backward_deterministic(case):
+def test_embedding_sorted_backward_deterministic(case, dt):
     """nd_embedding_bwd_sorted (stable argsort, 64-row chunks + ordered join of the runs that cross
     chunks) equals the index_add reference and is bitwise repeatable: heavily repeated ids (one id
     takes 25 % of the rows), a left-padded batch (6000 pad rows of one id, out-of-range ids skipped),
@@ -576,7 +579,7 @@ def test_embedding_sorted_backward_deterministic(case):
         ids = torch.repeat_interleave(torch.arange(0, 200, device=DEV),
                                       torch.tensor([64, 1, 63, 128, 65, 127] * 33 + [5, 9], device=DEV))[:n]
         n = ids.numel()
-    dy = torch.randn(n, d, device=DEV)
+    dy = torch.randn(n, d, device=DEV).to(dt)
     base = torch.randn(V, d, device=DEV)
     outs = []
     for _ in range(2):
@@ -584,12 +587,12 @@ def test_embedding_sorted_backward_deterministic(case):
         perm = torch.argsort(ids, stable=True)
         sid = ids.index_select(0, perm).contiguous()
         ws = sorted_bwd_workspace(n, d, DEV).fill_(float("nan"))  # partials must be fully written
-        _ext.check(_ext.lib().nd_embedding_bwd_sorted(sid.data_ptr(), perm.data_ptr(), dy.data_ptr(), gW.data_ptr(),
-                                                      ws.data_ptr(), n, d, V, _ext.stream_ptr()), "sorted")
+        _ext.check(_ext.lib().nd_embedding_bwd_sorted(sid.data_ptr(), perm.data_ptr(), dy.data_ptr(), _ext.dtcode(dy),
+                                                      gW.data_ptr(), ws.data_ptr(), n, d, V, _ext.stream_ptr()), "sorted")
         outs.append(gW)
     assert torch.equal(outs[0], outs[1])
     ok = (ids >= 0) & (ids < V)
-    ref_gw = base.double().index_add_(0, ids[ok], dy[ok].double())
+    ref_gw = base.double().index_add_(0, ids[ok], dy[ok].double())  # bf16 dy: exact in double
     assert torch.allclose(outs[0].double(), ref_gw, atol=1e-3, rtol=1e-5)
 
 

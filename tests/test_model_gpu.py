@@ -42,17 +42,22 @@ def test_hip_vs_torch_model(kv):
 
 @pytest.mark.parametrize("fp8", [False, True])
 def test_bf16_residual_model_tracks_fp32(fp8):
-    """--residual-dtype bf16 (HIP, bf16 compute, optionally fp8 projections) against the fp32 torch model:
-    the same tolerances as the fp32-residual HIP model."""
+    """--residual-dtype bf16 (HIP, bf16 compute, optionally fp8 projections) against the fp32 torch model: the
+    loss within the fp32-residual HIP model's tolerance, the gradient error at most a little above the
+    fp32-residual HIP model's own error (fp8: ~0.1 relative to fp32 either way)."""
     cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=512, num_attention_heads=4,
                                      num_key_value_heads=2, num_hidden_layers=2, vocab_size=1000,
                                      rms_norm_eps=1e-5))
-    ids = torch.randint(0, 1000, (2, 256), device="cuda")
+    ids = torch.randint(0, 1000, (2, 256), generator=torch.Generator().manual_seed(1)).cuda()
     l_t, g_t = _run(cfg, "torch", ids, torch.float32)
-    l_h, g_h = _run(cfg, "hip", ids, torch.bfloat16, residual_dtype=torch.bfloat16, fp8=fp8)
-    assert abs(l_t - l_h) < 2e-2 * abs(l_t)
-    rel = ((g_t - g_h).norm() / g_t.norm()).item()
-    assert rel < (1e-1 if fp8 else 5e-2), rel
+    rels = {}
+    for rdt in (torch.float32, torch.bfloat16):
+        l_h, g_h = _run(cfg, "hip", ids, torch.bfloat16, residual_dtype=rdt, fp8=fp8)
+        assert abs(l_t - l_h) < 2e-2 * abs(l_t), (rdt, l_t, l_h)
+        rels[rdt] = ((g_t - g_h).norm() / g_t.norm()).item()
+    assert rels[torch.bfloat16] < 1.25 * rels[torch.float32] + 1e-2, rels
+    if not fp8:
+        assert rels[torch.bfloat16] < 5e-2, rels
 
 
 @pytest.mark.parametrize("res", ["fp32", "bf16"])
