@@ -124,20 +124,22 @@ def test_smoke_entry():
     g.smoke()
 
 
-def test_hip_graph_matches_eager():
-    """Captured micro-step replays == eager micro-steps (gradients accumulate in the flat buffer)."""
+@pytest.mark.parametrize("rdt", [torch.float32, torch.bfloat16])
+def test_hip_graph_matches_eager(rdt):
+    """Captured micro-step replays == eager micro-steps (gradients accumulate in the flat buffer); fp32 and bf16
+    residual streams."""
     from nanodiloco_amd.utils.graphs import GraphedMicroStep
     ops.set_backend("hip")
     cfg = LlamaConfig.from_dict(dict(hidden_size=256, intermediate_size=512, num_attention_heads=4,
                                      num_key_value_heads=2, num_hidden_layers=2, vocab_size=1000))
     batches = [torch.randint(0, 1000, (2, 256), device="cuda") for _ in range(5)]
-    m1 = LlamaForCausalLM(cfg, "cuda", torch.bfloat16).init_weights(3)
+    m1 = LlamaForCausalLM(cfg, "cuda", torch.bfloat16, residual_dtype=rdt).init_weights(3)
     losses1 = []
     for ids in batches:
         out = m1(ids, labels=ids, loss_scale=0.2)
         out.loss.backward()
         losses1.append(out.loss.item())
-    m2 = LlamaForCausalLM(cfg, "cuda", torch.bfloat16).init_weights(3)
+    m2 = LlamaForCausalLM(cfg, "cuda", torch.bfloat16, residual_dtype=rdt).init_weights(3)
     g = GraphedMicroStep(m2)
     losses2 = [g(ids, ids, 0.2).item() for ids in batches]  # 2 eager warm-ups, capture, 3 replays
     torch.cuda.synchronize()
