@@ -136,3 +136,20 @@ def test_residual_dtype_auto():
     assert _residual_dtype("bf16") == torch.bfloat16
     with pytest.raises(ValueError):
         _residual_dtype("fp16")
+
+
+def test_trainer_runs_with_bf16_residual(tmp_path):
+    """--residual-dtype bf16 through the trainer (CPU, synthetic data): DiLoCo inner + outer steps run and the
+    model carries the bf16 residual stream."""
+    import torch
+
+    from nanodiloco_amd.trainer import TrainArgs, Trainer
+    cfg = tmp_path / "m.json"
+    cfg.write_text('{"hidden_size": 32, "intermediate_size": 64, "num_attention_heads": 2, '
+                   '"num_hidden_layers": 1, "vocab_size": 32}')
+    t = Trainer(TrainArgs(batch_size=4, per_device_batch_size=2, seq_length=16, warmup_steps=1, total_steps=4,
+                          inner_steps=2, llama_config_file=str(cfg), wandb="off", device="cpu", data="synthetic",
+                          residual_dtype="bf16"))
+    assert t.model.residual_dtype == torch.bfloat16
+    out = t.train()
+    assert out["steps"] == 4 and out["outer_steps"] == 2
