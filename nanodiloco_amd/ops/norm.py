@@ -173,6 +173,8 @@ class AddRMSNormFn(torch.autograd.Function):
             hn, w, rstd = ctx.saved_tensors
             dres = _rows(dhn).contiguous() if dhn is not None else None
             dx, da = _hip_bwd(dy, hn, w, rstd, dres, ctx.gw, ctx.a_dtype, ctx.q8_bwd)
+            # bf16 residual: dx and da are ONE tensor; both consumers (the previous norm's dres, the projection's
+            # dgrad / wgrad) only read it, and neither input is used twice, so autograd never accumulates into it
             return dx.view(ctx.shape), da.view(ctx.shape), None, None, None, None, None, None
         hn, w = ctx.saved_tensors
         dx, dw = ref.rmsnorm_backward(dy, hn, w, ctx.eps)
