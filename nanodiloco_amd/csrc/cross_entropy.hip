@@ -93,11 +93,14 @@ __global__ void __launch_bounds__(256) ce_reg_kernel(void* __restrict__ logits, 
 // fp32), so more waves fit per SIMD to keep the 64-KiB row loads in flight; scores are handled in
 // the log2 domain (one FMA + v_exp_f32 per element and pass); the target column is fixed up once by
 // the thread that owns it instead of a compare per element.
-template <int CH>
+// QF >= 0 (fp8 lm head, round 5): the dlogits go out ONLY as fp8 (QF: 0 e4m3, 1 e5m2) into q8.q [rows, V], from
+// the bf16-rounded values -- bitwise nd_fp8_cast over the bf16 dlogits, whose 4.2 GB write and re-read per
+// 65,536-row chunk this removes; amax partials as the other fused producers (common.h Fp8Out).
+template <int CH, int QF = -1>
 __global__ void __launch_bounds__(256) ce_bf16_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
                                                       float* __restrict__ loss_sum, const float* __restrict__ scale_p,
                                                       int V, int ignore, float* __restrict__ lse_out,
-                                                     float* __restrict__ row_loss) {
+                                                     float* __restrict__ row_loss, Fp8Out q8) {
   constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
   __shared__ float red[8];
   const int64_t row = blockIdx.x;
@@ -138,6 +141,8 @@ __global__ void __launch_bounds__(256) ce_bf16_kernel(bf16_t* __restrict__ logit
 #pragma unroll
   for (int c = 0; c < CH; ++c) asm volatile("" : "+v"(x[c].x), "+v"(x[c].y), "+v"(x[c].z), "+v"(x[c].w));
   const float sc = valid ? scale_p[0] : 0.f;
+  const float qsc = QF >= 0 ? q8.scale[0] : 1.f;
+  float qmax = 0.f;
   float picked = 0.f;
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
@@ -161,9 +166,20 @@ __global__ void __launch_bounds__(256) ce_bf16_kernel(bf16_t* __restrict__ logit
       }
       uint4 w;
       w.x = pack2(o[0], o[1]); w.y = pack2(o[2], o[3]); w.z = pack2(o[4], o[5]); w.w = pack2(o[6], o[7]);
-      *reinterpret_cast<uint4*>(rp + col) = w;
+      if constexpr (QF < 0) {
+        *reinterpret_cast<uint4*>(rp + col) = w;
+      } else {
+        const float r[8] = {lo_bf(w.x), hi_bf(w.x), lo_bf(w.y), hi_bf(w.y), lo_bf(w.z), hi_bf(w.z), lo_bf(w.w), hi_bf(w.w)};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qmax = fmaxf(qmax, fabsf(r[j]));
+        uint2 o8;
+        o8.x = cvt4<QF>(r[0] * qsc, r[1] * qsc, r[2] * qsc, r[3] * qsc);
+        o8.y = cvt4<QF>(r[4] * qsc, r[5] * qsc, r[6] * qsc, r[7] * qsc);
+        *reinterpret_cast<uint2*>(q8.q + row * (int64_t)V + col) = o8;
+      }
     }
   }
+  if constexpr (QF >= 0) block_amax_commit<256>(qmax, q8.amax, q8.parts);
   const float lse = lse2 * LN2;
   if (threadIdx.x == 0 && lse_out) lse_out[row] = lse;
   __syncthreads();
@@ -237,7 +253,8 @@ ND_API int nd_ce_fwd_bwd(void* logits, int dt, const int64_t* targets, float* lo
       else hipLaunchKernelGGL((ce_reg_kernel<F32, 4>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
     } else {
       if (dt == BF16 && !g_ce_reg)
-        hipLaunchKernelGGL((ce_bf16_kernel<16>), g, b, 0, s, (bf16_t*)logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
+        hipLaunchKernelGGL((ce_bf16_kernel<16>), g, b, 0, s, (bf16_t*)logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss,
+                           Fp8Out{nullptr, nullptr, nullptr, 1, 0});
       else if (dt == BF16) hipLaunchKernelGGL((ce_reg_kernel<BF16, 16>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
       else hipLaunchKernelGGL((ce_reg_kernel<F32, 16>), g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
     }
@@ -245,5 +262,27 @@ ND_API int nd_ce_fwd_bwd(void* logits, int dt, const int64_t* targets, float* lo
     if (dt == BF16) hipLaunchKernelGGL(ce_generic_kernel<BF16>, g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
     else hipLaunchKernelGGL(ce_generic_kernel<F32>, g, b, 0, s, logits, targets, loss_sum, scale, V, ignore, lse_out, row_loss);
   }
+  ND_LAUNCH_CHECK();
+}
+
+// fp8 lm head: the same loss / gradient with the dlogits written only as fp8 (q: [n, V] bytes; e4m3 or e5m2 by fmt,
+// qscale = device scalar, amax = `parts` partial maxima).  Only the packed bf16 kernel's shapes (V % 8 == 0,
+// 8192 < V <= 32768, bf16 logits); anything else returns hipErrorInvalidValue and the caller casts separately.
+// The logits buffer is left as the forward wrote it.
+ND_API int nd_ce_fwd_bwd_q8(void* logits, int dt, const int64_t* targets, float* loss_sum, const float* scale,
+                            int64_t n, int V, int ignore, float* lse_out, float* row_loss, void* q, const float* qscale,
+                            float* amax, int parts, int fmt, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (dt != BF16 || V % 8 != 0 || V <= 256 * 8 * 4 || V > 256 * 8 * 16 || g_ce_reg || !q || !qscale || !amax ||
+      parts < 1 || (fmt != 0 && fmt != 1))
+    return (int)hipErrorInvalidValue;
+  const Fp8Out q8{(uint8_t*)q, qscale, amax, parts, fmt};
+  dim3 g((unsigned)n), b(256);
+  if (fmt == 0)
+    hipLaunchKernelGGL((ce_bf16_kernel<16, 0>), g, b, 0, s, (bf16_t*)logits, targets, loss_sum, scale, V, ignore, lse_out,
+                       row_loss, q8);
+  else
+    hipLaunchKernelGGL((ce_bf16_kernel<16, 1>), g, b, 0, s, (bf16_t*)logits, targets, loss_sum, scale, V, ignore, lse_out,
+                       row_loss, q8);
   ND_LAUNCH_CHECK();
 }

@@ -154,6 +154,7 @@ def _declare(L: ctypes.CDLL):
         "nd_swiglu_bwd_q": [P, P, P, L64, I, P, P, P, I, I, P],
         # loss
         "nd_ce_fwd_bwd": [P, I, P, P, P, L64, I, I, P, P, F, P],
+        "nd_ce_fwd_bwd_q8": [P, I, P, P, P, L64, I, I, P, P, P, P, P, I, I, P],
         # embedding
         "nd_embedding_fwd": [P, P, P, I, L64, I, I, P],
         "nd_embedding_bwd": [P, P, I, P, L64, I, I, P],

@@ -16,8 +16,9 @@ so only one chunk of logits ever exists and nothing [N, V]-sized survives the fo
 ``s = loss_scale / n_valid`` is read from device memory (no host sync).
 
 fp8 (``f8`` = the model's ``Fp8Linears``, BASELINE config 5): the three GEMMs run on the own fp8 kernels --
-logits = e4m3 y8 . W8^T, the CE kernel's bf16 dlogits are cast once to e5m2 (delayed scaling, slot
-"x.lm"), dy = dlogits8 . (W^T)8^T and gW += dlogits8^T y8 (wgrad8_pp_kernel).  The returned loss is the
+logits = e4m3 y8 . W8^T, the CE kernel writes the dlogits straight as e5m2 (delayed scaling, slot "x.lm";
+``nd_ce_fwd_bwd_q8``, bitwise the bf16 dlogits + separate cast that the first step, which has no scale yet,
+still takes), dy = dlogits8 . (W^T)8^T and gW += dlogits8^T y8 (wgrad8_pp_kernel).  The returned loss is the
 unscaled mean over valid tokens (ignore_index=-100), matching ``HF/loss/loss_utils.py:32-71``.
 
 Contract: the weight gradient is produced in the forward, assuming the loss is back-propagated
@@ -36,6 +37,7 @@ from .determinism import deterministic
 from .linear import mm_nt, wgrad_accumulate
 
 IGNORE_INDEX = -100
+_HIP_INVALID_VALUE = 1  # hipErrorInvalidValue: a launcher refused the shape (caller takes the general path)
 
 
 # logits chunk budget (ND_CE_CHUNK_MB, default 4 GiB: a whole 64k-token micro-batch of a 32k
@@ -86,14 +88,29 @@ class LMHeadCEFn(torch.autograd.Function):
                 else:  # the selected plain projection GEMM (ops/linear.py proj_gemm: hipBLASLt by default)
                     logits = mm_nt(yc, w)
                 rows = torch.empty(e - s, dtype=torch.float32, device=y.device) if det else None
-                _ext.check(_ext.lib().nd_ce_fwd_bwd(_ext.ptr(logits), _ext.dtcode(logits), _ext.ptr(tc),
-                                                    _ext.ptr(loss_sum), _ext.ptr(scale), e - s, V, IGNORE_INDEX,
-                                                    0, _ext.ptr(rows) if det else 0, 0.0,
-                                                    _ext.stream_ptr(y.device)), "nd_ce_fwd_bwd")
+                dl8 = None
+                t8 = q[0].target(q[2], E5M2) if q is not None else None
+                if t8 is not None:
+                    # fp8: the CE kernel writes the e5m2 dlogits itself (no bf16 dlogits, no separate cast)
+                    q8 = t8.alloc((e - s, V), y.device)
+                    rc = _ext.lib().nd_ce_fwd_bwd_q8(_ext.ptr(logits), _ext.dtcode(logits), _ext.ptr(tc),
+                                                     _ext.ptr(loss_sum), _ext.ptr(scale), e - s, V, IGNORE_INDEX, 0,
+                                                     _ext.ptr(rows) if det else 0, *t8.args(q8),
+                                                     _ext.stream_ptr(y.device))
+                    if rc == 0:
+                        dl8 = q8
+                    elif rc != _HIP_INVALID_VALUE:  # invalid value = shape not taken: cast separately below
+                        _ext.check(rc, "nd_ce_fwd_bwd_q8")
+                if dl8 is None:
+                    _ext.check(_ext.lib().nd_ce_fwd_bwd(_ext.ptr(logits), _ext.dtcode(logits), _ext.ptr(tc),
+                                                        _ext.ptr(loss_sum), _ext.ptr(scale), e - s, V, IGNORE_INDEX,
+                                                        0, _ext.ptr(rows) if det else 0, 0.0,
+                                                        _ext.stream_ptr(y.device)), "nd_ce_fwd_bwd")
                 if det:  # per-row losses, one ordered reduction (no float atomics)
                     loss_sum += rows.sum()
-                dl = logits
+                dl = logits if dl8 is None else None
             else:
+                dl8 = None
                 logits = torch.mm(yc.float(), w.float().t())
                 lse = torch.logsumexp(logits, dim=-1)
                 ok = tc != IGNORE_INDEX
@@ -107,8 +124,9 @@ class LMHeadCEFn(torch.autograd.Function):
             if q is not None:
                 # e5m2 dlogits (one cast; delayed scaling of slot kdy), then both gradient GEMMs in fp8
                 r, kx, kdy, y8, wq = q
-                r._first_use(dl, kdy)
-                dl8 = cast(dl, r.scale[kdy:kdy + 1], E5M2, r.amax[kdy])
+                if dl8 is None:
+                    r._first_use(dl, kdy)
+                    dl8 = cast(dl, r.scale[kdy:kdy + 1], E5M2, r.amax[kdy])
                 gemm_pp_f8(dl8, wq.wT8, r.inv[kdy:kdy + 1], wq.inv, out=dy[s:e])
                 if gw is not None:
                     _wgrad_f8(gw, dl8, y8[s:e], r.inv[kdy:kdy + 1], r.inv[kx:kx + 1], dl)

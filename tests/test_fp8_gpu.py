@@ -189,6 +189,52 @@ def test_fused_swiglu_quant_bitwise(fmt):
     assert rb.amax[kb].max().item() == dgu.float().abs().max().item()
 
 
+@pytest.mark.parametrize("V", [32000, 16384])
+def test_ce_fused_fp8_dlogits_bitwise(V):
+    """nd_ce_fwd_bwd_q8 (the CE kernel writing the dlogits only as e5m2) == the bf16 CE kernel + a separate
+    cast: fp8 bytes and amax bitwise, loss within float-atomic order; the logits buffer is left untouched."""
+    from nanodiloco_amd.ops import _ext
+    n = 1000
+    logits = (3 * torch.randn(n, V, device="cuda")).bfloat16()
+    tgt = torch.randint(0, V, (n,), device="cuda")
+    tgt[::9] = -100
+    scale = torch.tensor([1.0 / 800], device="cuda")
+    L = _ext.lib()
+    # reference: bf16 dlogits in place, then the separate cast
+    ref_l = logits.clone()
+    loss_ref = torch.zeros(1, device="cuda")
+    _ext.check(L.nd_ce_fwd_bwd(ref_l.data_ptr(), _ext.dtcode(ref_l), tgt.data_ptr(), loss_ref.data_ptr(),
+                               scale.data_ptr(), n, V, -100, 0, 0, 0.0, _ext.stream_ptr()), "ce")
+    r, k, t = _target(fp8.E5M2, 2000.0)
+    ref8 = fp8.cast(ref_l, r.scale[k:k + 1], fp8.E5M2)
+    # fused
+    r2, k2, t2 = _target(fp8.E5M2, 2000.0)
+    q8 = t2.alloc((n, V), "cuda")
+    fl = logits.clone()
+    loss = torch.zeros(1, device="cuda")
+    _ext.check(L.nd_ce_fwd_bwd_q8(fl.data_ptr(), _ext.dtcode(fl), tgt.data_ptr(), loss.data_ptr(), scale.data_ptr(),
+                                  n, V, -100, 0, 0, *t2.args(q8), _ext.stream_ptr()), "ce_q8")
+    torch.cuda.synchronize()
+    assert torch.equal(fl, logits)
+    assert torch.equal(q8.view(torch.uint8), ref8.view(torch.uint8))
+    assert r2.amax[k2].max().item() == ref_l.float().abs().max().item()
+    assert abs(loss.item() - loss_ref.item()) <= 1e-5 * abs(loss_ref.item())
+
+
+def test_ce_fused_fp8_refuses_other_shapes():
+    """Shapes outside the packed kernel's range come back as hipErrorInvalidValue (the caller casts separately)."""
+    from nanodiloco_amd.ops import _ext
+    n, V = 8, 1000
+    logits = torch.randn(n, V, device="cuda").bfloat16()
+    tgt = torch.randint(0, V, (n,), device="cuda")
+    r, k, t = _target(fp8.E5M2)
+    q8 = t.alloc((n, V), "cuda")
+    loss, scale = torch.zeros(1, device="cuda"), torch.ones(1, device="cuda")
+    rc = _ext.lib().nd_ce_fwd_bwd_q8(logits.data_ptr(), _ext.dtcode(logits), tgt.data_ptr(), loss.data_ptr(),
+                                     scale.data_ptr(), n, V, -100, 0, 0, *t.args(q8), _ext.stream_ptr())
+    assert rc == 1
+
+
 @pytest.mark.parametrize("hdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("residual", [False, True])
 def test_fused_rmsnorm_quant_bitwise(residual, hdt):
