@@ -365,6 +365,39 @@ def test_fp8_lm_head_tracks_bf16_one_step():
     assert rel(gf, gb) < 0.15 and rel(wf, wb) < 0.15, (rel(gf, gb), rel(wf, wb))
 
 
+def test_fp8_lm_head_fused_dlogits_match_separate_cast():
+    """V = 32000 (the packed CE kernel's range): from the second call on (the slot has a scale), the CE kernel
+    writes the e5m2 dlogits itself; loss, input gradient and weight gradient are bitwise those of the separate
+    cast path (fused quantisation off), and so is the slot's amax."""
+    from nanodiloco_amd.ops.cross_entropy import LM_KEY, lm_head_ce
+    from nanodiloco_amd.ops.linear import join_wgrad
+    torch.manual_seed(0)
+    n, d, V = 512, 256, 32000
+    y = (torch.randn(n, d, device="cuda") * 0.5).bfloat16()
+    w = (torch.randn(V, d, device="cuda") * 0.05).bfloat16()
+    t = torch.randint(0, V, (n,), device="cuda")
+    t[::11] = -100
+    outs = []
+    for fused in (True, False):
+        fp8.set_fused_quant(fused)
+        try:
+            lin = fp8.Fp8Linears("cuda", wgrad_fp8=True)
+            for _ in range(2):
+                gw = torch.zeros(V, d, device="cuda")
+                yy = y.clone().requires_grad_(True)
+                loss = lm_head_ce(yy, w, gw, t, 1.0, f8=(lin, 0, None))
+                loss.backward()
+                join_wgrad()
+            torch.cuda.synchronize()
+            kdy = lin._slots(LM_KEY)[1]
+            outs.append((loss.item(), yy.grad.clone(), gw.clone(), lin.recipe.amax[kdy].max().item()))
+        finally:
+            fp8.set_fused_quant(True)
+    (l1, g1, w1, a1), (l2, g2, w2, a2) = outs
+    assert abs(l1 - l2) <= 1e-5 * abs(l2)
+    assert torch.equal(g1, g2) and torch.equal(w1, w2) and a1 == a2
+
+
 def _fp8_model_steps(cfg, ids, steps, overlap=None, fused=None):
     """A few fp8 training steps (fp8 weight gradients); returns (per-step flat grads, final master weights)."""
     prev_ov = ops.wgrad_overlap_enabled()
