@@ -8,9 +8,9 @@ statistics, the residual gradient is bf16 and doubles as the branch gradient (do
 
 Forward, HIP path: one kernel, one row per wave (``nd_rmsnorm_fwd``) fusing
 ``h_new = h + a`` (K8) with ``y = w * h_new * rstd`` (K2) and saving ``rstd``.
-Backward: one kernel producing dx (fp32, already summed with the incoming residual grad) and the
-branch grad in the compute dtype, plus per-block dw partials that are reduced into the flat
-grad buffer.
+Backward: one kernel producing dx (in the residual dtype, already summed with the incoming residual
+grad) and the branch grad in the compute dtype (the same tensor as dx for a bf16 residual), plus
+per-block dw partials that are reduced into the flat grad buffer.
 """
 from __future__ import annotations
 
