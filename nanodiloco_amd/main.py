@@ -61,8 +61,10 @@ def main(argv: Optional[List[str]] = None):
     args = parse_args(argv if argv is not None else sys.argv[1:])
     try:
         Trainer(args).train()
-    finally:
-        destroy_distributed()
+    except BaseException:
+        destroy_distributed(abort=True)
+        raise
+    destroy_distributed()
 
 
 if __name__ == "__main__":

@@ -106,6 +106,12 @@ class FlatCommunicator:
             from .rccl import communicator_for
             self.rccl = communicator_for(group, device, timeout_s)
 
+    def check(self, what: str = "step boundary"):
+        """Raise if the own RCCL communicator failed (see :meth:`parallel.rccl.RcclCommunicator.check`).
+        c10d collectives raise from ``Work.wait`` themselves."""
+        if self.rccl is not None:
+            self.rccl.check(what)
+
     def all_reduce_async(self, flat: torch.Tensor, ranges: Optional[Sequence[Range]] = None) -> PendingAllReduce:
         if ranges is None:
             ranges = plan_buckets(0, flat.numel(), flat.element_size(), self.bucket_bytes)

@@ -228,6 +228,9 @@ class Diloco:
                                first, drift_base=self.drift_base[x:y] if self.overlap else None)
         opt.step_count += 1
         self.store.version += 1
+        # own RCCL: a watchdog abort still completes the collective's event, so the update above may have
+        # consumed a partial reduction -- fail before anything builds on it (c10d raises in Work.wait)
+        self.outer_comm.check("the outer update")
         if self.env.inner_dp > 1:
             # every GPU of the worker updated its shard; replicate master and snapshot
             self.inner_comm.all_gather_flat(master, self.shards, self.env.inner_rank)

@@ -67,6 +67,7 @@ class InnerGradSync:
         self._pending.append(self.comm.all_reduce_async(grad, spans))
         for p in self._pending:
             p.wait_all()
+        self.comm.check("the inner-DDP gradient is used")
         self.last_hook_count = len(self._hooked)
         self._pending = []
         self._armed = False

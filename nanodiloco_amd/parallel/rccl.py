@@ -12,8 +12,15 @@ Here each process group that carries DiLoCo traffic gets its own ``ncclComm_t``:
 * collectives run in place on the communicator's own high-priority HIP stream, ordered after the
   producer stream's queued work by an event; ``wait(ticket)`` makes a consumer stream wait on the GPU
   (the host never blocks);
+* the communicator is non-blocking: ``ncclCommInitRankConfig`` waits for the other members at most
+  ``init_timeout_s`` (a member that never joins -> :class:`RcclError`, not a hang);
 * a watchdog thread in the library aborts the communicator when a collective outlives the collective
-  timeout or RCCL reports an asynchronous error; every later call raises :class:`RcclError`.
+  timeout or RCCL reports an asynchronous error; every later call raises :class:`RcclError`, and
+  :meth:`RcclCommunicator.check` raises it at the step boundaries that KEEP reduced data (the outer
+  update, the inner-DDP gradient, a checkpoint): an aborted collective's completion event still fires, so
+  without the check a partially reduced buffer could reach the weights or a checkpoint;
+* ``destroy(abort=True)`` (an exception is propagating) aborts at once; a normal destroy drains the
+  communicator stream within the collective timeout and aborts if that fails.
 
 The torch process group stays for the control plane (barriers, the bench's MAX reduction, the debug
 replica checksums); the bulk traffic -- initial broadcast, outer all-reduce buckets, inner-DDP gradient
@@ -61,7 +68,9 @@ def lib() -> ctypes.CDLL:
                     "nd_comm_unique_id_bytes": [],
                     "nd_comm_get_unique_id": [P],
                     "nd_comm_init": [ctypes.POINTER(P), I, P, I, I, I, ctypes.c_double],
+                    "nd_comm_init2": [ctypes.POINTER(P), I, P, I, I, I, ctypes.c_double, ctypes.c_double],
                     "nd_comm_destroy": [P],
+                    "nd_comm_destroy2": [P, I],
                     "nd_comm_abort": [P],
                     "nd_comm_all_reduce": [P, P, P, SZ, I, I, P, ctypes.POINTER(L64)],
                     "nd_comm_broadcast": [P, P, SZ, I, I, P, ctypes.POINTER(L64)],
@@ -105,7 +114,7 @@ class RcclCommunicator:
     """One ``ncclComm_t`` for the members of ``group`` (torch process group or None = WORLD)."""
 
     def __init__(self, group, device: torch.device, timeout_s: float = 1800.0, high_priority: bool = True,
-                 store=None):
+                 store=None, init_timeout_s: Optional[float] = None):
         L = lib()
         self.device = device
         self.ranks = _group_ranks(group)
@@ -131,9 +140,12 @@ class RcclCommunicator:
         dev_index = device.index if device.type == "cuda" and device.index is not None else 0
         if os.environ.get("ND_COMM_PRIORITY", "high") == "normal":  # A/B of the stream priority
             high_priority = False
-        _check(L.nd_comm_init(ctypes.byref(self._h), self.size, idbuf, self.rank, dev_index, int(high_priority),
-                              float(timeout_s)), f"ncclCommInitRank({key})")
         self.key = key
+        rc = L.nd_comm_init2(ctypes.byref(self._h), self.size, idbuf, self.rank, dev_index, int(high_priority),
+                             float(timeout_s), float(init_timeout_s if init_timeout_s is not None else timeout_s))
+        if rc != 0:
+            self._h = None
+            _check(rc, f"ncclCommInitRankConfig({key})")
 
     # ------------------------------------------------------------------ collectives (in place, async)
     def all_reduce(self, t: torch.Tensor) -> int:
@@ -180,15 +192,25 @@ class RcclCommunicator:
         return {"calls": calls.value, "bytes": nbytes.value, "stream": stream.value, "priority": prio.value}
 
     def error(self) -> int:
-        return lib().nd_comm_error(self._h)
+        return lib().nd_comm_error(self._h) if self._h is not None else 0
+
+    def check(self, what: str = "step boundary"):
+        """Raise if the communicator has failed (watchdog timeout, async RCCL error, abort).  Called where
+        reduced data is about to be kept: an aborted collective still completes its event, so the GPU-side
+        waits alone cannot tell a full reduction from a partial one."""
+        rc = self.error()
+        if rc != 0:
+            raise RcclError(f"rccl communicator {self.key} failed before {what}: "
+                            f"{lib().nd_comm_error_string(rc).decode()} (code {rc})")
 
     def abort(self):
         if self._h is not None:
             lib().nd_comm_abort(self._h)
 
-    def destroy(self):
+    def destroy(self, abort: bool = False):
+        """``abort``: an exception is propagating (or a peer is known dead): no drain, abort at once."""
         if self._h is not None and self._h.value:
-            lib().nd_comm_destroy(self._h)
+            lib().nd_comm_destroy2(self._h, int(abort))
         self._h = None
 
     def __del__(self):  # best effort; processes normally call destroy_communicators() first
@@ -212,9 +234,9 @@ def communicator_for(group, device: torch.device, timeout_s: float = 1800.0,
     return c
 
 
-def destroy_communicators():
+def destroy_communicators(abort: bool = False):
     for c in list(_COMMS.values()):
-        c.destroy()
+        c.destroy(abort)
     _COMMS.clear()
 
 

@@ -22,8 +22,8 @@ class _FakeLib:
         self.rank, self.n, self.inits = rank, 0, []
         self.nd_comm_unique_id_bytes = _FakeFn(lambda: 128)
         self.nd_comm_get_unique_id = _FakeFn(self._uid)
-        self.nd_comm_init = _FakeFn(self._init)
-        self.nd_comm_destroy = _FakeFn(lambda h: 0)
+        self.nd_comm_init2 = _FakeFn(self._init)
+        self.nd_comm_destroy2 = _FakeFn(lambda h, abort: 0)
 
     def _uid(self, buf):
         self.n += 1
@@ -31,7 +31,7 @@ class _FakeLib:
         ctypes.memmove(buf, raw, 128)
         return 0
 
-    def _init(self, handle, nranks, idbuf, rank, device, hp, timeout):
+    def _init(self, handle, nranks, idbuf, rank, device, hp, timeout, init_timeout):
         self.inits.append((nranks, rank, bytes(idbuf.raw).rstrip(b"\0").decode()))
         handle._obj.value = 1
         return 0

@@ -9,7 +9,7 @@ import sys
 import pytest
 import torch
 
-from ._mp import free_port
+from ._mp import child_env, free_port
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -22,14 +22,14 @@ def _gpu(hip_lib):
 
 
 def test_rccl_one_rank_collectives_diloco_and_hooks():
-    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+    env = child_env(OMP_NUM_THREADS="4")
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "_rccl_check.py")], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "RCCL_CHECK_PASSED" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
 
 
 def test_bench_torchrun_one_rank_nccl():
-    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+    env = child_env(OMP_NUM_THREADS="4")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "1", "--backend", "nccl",
            "--model", "llama_tiny.json", "--batch-size", "16", "--micro-batch", "8", "--seq-len", "256",
@@ -49,7 +49,7 @@ def test_bench_torchrun_one_rank_nccl():
 def test_bench_default_one_gpu_runs_rccl_path():
     """``python bench.py`` with no backend flag (the driver's 1-GPU headline) creates the one-rank RCCL group and
     issues the outer step's bucketed all-reduce on the own communicator (verdict r4 item 5)."""
-    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+    env = child_env(OMP_NUM_THREADS="4")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID"):
         env.pop(k, None)
     cmd = [sys.executable, "bench.py", "--model", "llama_tiny.json", "--batch-size", "16", "--micro-batch", "8",
@@ -60,3 +60,16 @@ def test_bench_default_one_gpu_runs_rccl_path():
     assert j["comm_backend"] == "nccl" and j["comm_impl"] == "rccl", j
     assert j["allreduce_calls_per_outer_step"] >= 1 and j["rccl_calls"] >= 1 and j["outer_steps_in_window"] == 1
     assert j["outer_phase_ms"]["allreduce"] > 0
+
+
+def test_rccl_init_times_out_when_peer_never_joins():
+    """Verdict r5 item 3: a 2-rank communicator in which only rank 0 joins -- the non-blocking init returns the
+    timeout error within init_timeout + 5 s, the process keeps working (one-rank collectives, host abort,
+    abort-destroy, normal destroy) and exits cleanly."""
+    env = child_env(OMP_NUM_THREADS="4", ND_FAULT_INIT_TIMEOUT="6")
+    t0 = __import__("time").perf_counter()
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "_rccl_fault_check.py")], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=120)
+    dt = __import__("time").perf_counter() - t0
+    assert r.returncode == 0 and "RCCL_FAULT_CHECK_PASSED" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+    print(r.stdout[-1500:], f"(child {dt:.1f} s)")
