@@ -64,18 +64,64 @@ def _env_int(k, d):
     return int(v) if v not in (None, "") else d
 
 
-def _pg_options(backend: str, high_priority: bool):
+def _pg_options(backend: str, high_priority: bool, timeout: Optional[datetime.timedelta] = None):
     """RCCL process groups run their collectives on a HIGH-PRIORITY HIP stream: the
     bucketed outer all-reduce that ``--overlap-outer`` issues beside the next round's first inner step
     (and the inner-DDP gradient buckets beside the backward) is then scheduled ahead of the compute
-    queue's kernels when both are ready."""
+    queue's kernels when both are ready.  The options carry the group's timeout too (torch warns when an
+    options object's timeout differs from the ``timeout`` argument it then overrides it with)."""
     if backend != "nccl" or not high_priority or os.environ.get("ND_COMM_PRIORITY", "high") == "normal":
         return None
     try:
         from torch.distributed import ProcessGroupNCCL
     except ImportError:  # torch built without RCCL
         return None
-    return ProcessGroupNCCL.Options(is_high_priority_stream=True)
+    o = ProcessGroupNCCL.Options(is_high_priority_stream=True)
+    if timeout is not None:
+        o._timeout = timeout
+    return o
+
+
+def worker_group_namespace(store, rank: int, world: int, timeout_s: float = 300.0) -> str:
+    """A key namespace unique to THIS worker group, agreed by all its ranks through ``store``.
+
+    torchrun's agent store outlives the worker groups it starts: after a failure restart
+    (TORCHELASTIC_RESTART_COUNT + 1) and after a membership change of an elastic ``--nnodes=min:max`` job
+    (the count does NOT move), the new group sees every key the old one wrote -- gloo peer addresses, the
+    own RCCL communicators' unique ids -- and would read them.  Rank 0 of the group draws a fresh nonce and
+    hands it to every other rank through keys that cannot be stale:
+
+    * rank r counts its incarnations (``add("nd_ns/inc/r", 1)`` = i_r: a number no earlier process of rank
+      r had), points ``nd_ns/req/r`` at it and blocks on ``nd_ns/ans/r/<i_r>``, a key nothing wrote before;
+    * rank 0 answers whatever incarnation ``nd_ns/req/r`` points at, and repeats until rank r acknowledges
+      with rank 0's OWN nonce -- a leftover pointer or acknowledgement of a dead group carries another
+      nonce, so it is answered (harmlessly) but never taken for this group's.
+
+    World size may differ between groups and workers may have died at any point: nothing counts arrivals."""
+    import time
+    import uuid
+    deadline = time.monotonic() + timeout_s
+    inc = store.add(f"nd_ns/inc/{rank}", 1)
+    if rank == 0:
+        nonce = f"{inc}-{uuid.uuid4().hex[:12]}"
+        todo = set(range(1, world))
+        while todo:
+            for r in sorted(todo):
+                if not store.check([f"nd_ns/req/{r}"]):
+                    continue
+                i_r = store.get(f"nd_ns/req/{r}").decode()
+                store.set(f"nd_ns/ans/{r}/{i_r}", nonce)
+                if store.check([f"nd_ns/ack/{r}/{i_r}"]) and store.get(f"nd_ns/ack/{r}/{i_r}").decode() == nonce:
+                    todo.discard(r)
+            if todo:
+                if time.monotonic() > deadline:
+                    raise TimeoutError(f"worker-group namespace: ranks {sorted(todo)} never checked in")
+                time.sleep(0.005)
+        return nonce
+    store.set(f"nd_ns/req/{rank}", str(inc))
+    nonce = store.get(f"nd_ns/ans/{rank}/{inc}").decode()  # blocks (store timeout) until rank 0 answers
+    store.set(f"nd_ns/ack/{rank}/{inc}", nonce)
+    return nonce
 
 
 def comm_stream_high_priority(group=None) -> Optional[bool]:
@@ -156,21 +202,23 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
         kw = dict(backend=backend, timeout=timeout)
         if backend == "nccl":
             kw["device_id"] = dev  # eager RCCL communicator init
-            kw["pg_options"] = _pg_options(backend, high_priority)
+            kw["pg_options"] = _pg_options(backend, high_priority, timeout)
         launched = "TORCHELASTIC_RUN_ID" in os.environ and "MASTER_PORT" in os.environ
-        restart = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0)
         if world == 1 and not launched:
             # one rank outside torchrun: nothing to rendezvous with (a stray MASTER_ADDR without
             # MASTER_PORT / RANK must not send us into an env:// rendezvous)
             kw.update(store=dist.HashStore(), rank=0, world_size=1)
-        elif launched and restart > 0 and os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true":
-            # a torchrun --max-restarts restart: the static rendezvous keeps the agent's ONE TCPStore across
-            # attempts, while torch's env:// handler assumes a fresh store per attempt and adds no prefix
-            # (rendezvous._create_c10d_store), so the restarted workers would read attempt 0's keys (gloo
-            # peer addresses: "Connection refused").  Prefix this attempt's keys.
+        elif launched and os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true":
+            # torchrun's agent store is shared by every worker group it starts (failure restarts AND
+            # elastic membership changes, which do not move TORCHELASTIC_RESTART_COUNT), while torch's
+            # env:// handler assumes a fresh store per attempt and adds no prefix
+            # (rendezvous._create_c10d_store): a new group would read the old one's keys (gloo peer
+            # addresses: "Connection refused"; the own RCCL unique ids).  Every group, the first one
+            # included, works in a namespace of its own (worker_group_namespace).
             base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world, False,
                                  timeout=timeout)
-            kw.update(store=dist.PrefixStore(f"nd_restart_{restart}", base), rank=rank, world_size=world)
+            ns = worker_group_namespace(base, rank, world, timeout_s)
+            kw.update(store=dist.PrefixStore(f"nd_group_{ns}", base), rank=rank, world_size=world)
         dist.init_process_group(**kw)
     env.backend = backend
     env.comm_impl = _resolve_comm_impl(comm_impl, backend)
@@ -182,21 +230,23 @@ def init_distributed(backend: str = "auto", inner_dp: int = 1, device: Optional[
     else:
         for w in range(env.num_workers):  # every rank must create every group, in the same order
             ranks = list(range(w * inner_dp, (w + 1) * inner_dp))
-            g = dist.new_group(ranks, timeout=timeout, pg_options=_pg_options(backend, high_priority))
+            g = dist.new_group(ranks, timeout=timeout, pg_options=_pg_options(backend, high_priority, timeout))
             if w == env.worker:
                 env.inner_group = g
         if env.num_workers > 1:
             for r in range(inner_dp):
                 ranks = list(range(r, world, inner_dp))
-                g = dist.new_group(ranks, timeout=timeout, pg_options=_pg_options(backend, high_priority))
+                g = dist.new_group(ranks, timeout=timeout, pg_options=_pg_options(backend, high_priority, timeout))
                 if r == env.inner_rank:
                     env.outer_group = g
     return env
 
 
-def destroy_distributed():
+def destroy_distributed(abort: bool = False):
+    """``abort``: called while an exception propagates -- the own RCCL communicators abort instead of
+    draining (a collective may be waiting on a peer that will never arrive)."""
     from .rccl import destroy_communicators
-    destroy_communicators()
+    destroy_communicators(abort)
     if dist.is_initialized():
         dist.destroy_process_group()
 
