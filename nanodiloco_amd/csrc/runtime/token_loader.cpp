@@ -3,11 +3,16 @@
 // The reference tokenises the whole dataset on every rank at start-up and pads batches on the
 // training thread (REF/nanodiloco/training_utils/utils.py:45-55, REF/nanodiloco/main.py:79-96,
 // num_workers=0).  Here the corpus is pre-tokenised once into flat little-endian uint16/uint32
-// shard files; this loader memory-maps them (no copy, no parse), cuts fixed seq_len windows, gives
-// rank r the windows r, r+W, r+2W, ... (disjoint across DiLoCo workers), shuffles them per epoch
-// with a seeded Fisher-Yates permutation, and assembles int64 batches on a background thread into
-// a ring of caller-owned (pinned) host buffers.  The stream is a pure function of
-// (seed, rank, world, cursor), so checkpoints resume exactly.
+// shard files; this loader memory-maps them (no copy, no parse), cuts fixed seq_len windows and
+// assembles int64 batches on a background thread into a ring of caller-owned (pinned) host buffers.
+//
+// Sample order: ONE global stream of window positions q = 0, 1, 2, ... (epoch q / G, G = total
+// windows; window = perm_epoch(q mod G), a seeded Feistel permutation with cycle walking -- O(1)
+// memory, any G).  Rank r of W takes positions base + r, base + r + W, base + r + 2W, ...: the DiLoCo
+// workers' streams are disjoint inside every epoch and together consume the global stream in order.
+// The state is (base, W, cursor); all workers advance in lockstep, so the global position reached is
+// base + cursor * W.  An elastic resume on W' workers (utils/checkpoint.py) restarts every worker, old
+// and new, at base' = that position: no window is repeated and none skipped across the resize.
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -38,6 +43,39 @@ inline uint64_t splitmix64(uint64_t& s) {
   return z ^ (z >> 31);
 }
 
+// Bijection of [0, n) keyed by (seed, epoch): a 4-round balanced Feistel network on the smallest even
+// bit width covering n, with cycle walking (values >= n are permuted again; fewer than 4 steps expected).
+struct Perm {
+  uint64_t n = 1, mask = 1, key[4] = {0, 0, 0, 0};
+  int half = 1;
+  void init(uint64_t n_, uint64_t seed, uint64_t epoch) {
+    n = n_;
+    int bits = 2;
+    while (bits < 64 && (1ull << bits) < n) ++bits;
+    half = (bits + 1) / 2;
+    mask = (1ull << half) - 1;
+    uint64_t s = seed ^ (0xA24BAED4963EE407ull * (epoch + 1));
+    for (auto& k : key) k = splitmix64(s);
+  }
+  uint64_t once(uint64_t x) const {
+    uint64_t l = x >> half, r = x & mask;
+    for (int i = 0; i < 4; ++i) {
+      uint64_t h = r ^ key[i];
+      h = (h ^ (h >> 31)) * 0x7FB5D329728EA185ull;
+      h = (h ^ (h >> 27)) * 0x81DADEF4BC2DD44Dull;
+      const uint64_t nl = r, nr = (l ^ (h ^ (h >> 33))) & mask;
+      l = nl;
+      r = nr;
+    }
+    return (l << half) | r;
+  }
+  uint64_t operator()(uint64_t x) const {
+    do x = once(x);
+    while (x >= n);
+    return x;
+  }
+};
+
 struct Loader {
   std::vector<Shard> shards;
   int token_bytes = 2;
@@ -45,10 +83,11 @@ struct Loader {
   uint64_t seed = 0;
   int rank = 0, world = 1;
   bool shuffle = true;
-  int64_t my_windows = 0;        // windows owned by this rank per epoch
-  std::vector<int64_t> perm;     // permutation of [0, my_windows) for the current epoch
+  int64_t total_windows = 0;     // G: windows of the corpus, one epoch of the global stream
+  int64_t base = 0;              // global stream position this rank's cursor counts from
+  Perm perm;                     // window order of epoch perm_epoch
   int64_t perm_epoch = -1;
-  int64_t cursor = 0;            // samples handed out so far (monotonic across epochs)
+  int64_t cursor = 0;            // samples handed out since `base` (monotonic across epochs)
 
   // prefetch ring
   int nslots = 0;
@@ -76,17 +115,17 @@ struct Loader {
     if (worker.joinable()) worker.join();
   }
 
-  void build_perm(int64_t epoch) {
-    perm.resize(my_windows);
-    for (int64_t i = 0; i < my_windows; ++i) perm[i] = i;
-    if (shuffle) {
-      uint64_t s = seed ^ (0xA24BAED4963EE407ull * (uint64_t)(epoch + 1)) ^ (0x9FB21C651E98DF25ull * (uint64_t)(rank + 1));
-      for (int64_t i = my_windows - 1; i > 0; --i) {
-        int64_t j = (int64_t)(splitmix64(s) % (uint64_t)(i + 1));
-        std::swap(perm[i], perm[j]);
-      }
+  // global window of this rank's sample `sample` (counted from `base`); `pc` / `pe`: the caller's
+  // cached permutation and its epoch (the worker thread's own, or a local one)
+  int64_t window_of(int64_t sample, Perm& pc, int64_t& pe) const {
+    const int64_t q = base + rank + sample * (int64_t)world;
+    const int64_t epoch = q / total_windows, idx = q % total_windows;
+    if (!shuffle) return idx;
+    if (epoch != pe) {
+      pc.init((uint64_t)total_windows, seed, (uint64_t)epoch);
+      pe = epoch;
     }
-    perm_epoch = epoch;
+    return (int64_t)pc((uint64_t)idx);
   }
 
   void read_window(int64_t gw, int64_t* out) const {
@@ -106,15 +145,7 @@ struct Loader {
 
   // Fill `out` (batch*seq_len int64) with the samples starting at sample index `cur`.
   void fill(int64_t cur, int64_t* out) {
-    for (int64_t b = 0; b < batch; ++b) {
-      int64_t sample = cur + b;
-      int64_t epoch = sample / my_windows;
-      int64_t idx = sample % my_windows;
-      if (epoch != perm_epoch) build_perm(epoch);
-      int64_t local = perm[idx];
-      int64_t gw = local * world + rank;
-      read_window(gw, out + b * seq_len);
-    }
+    for (int64_t b = 0; b < batch; ++b) read_window(window_of(cur + b, perm, perm_epoch), out + b * seq_len);
   }
 
   void run() {
@@ -190,8 +221,8 @@ void* nd_loader_create(const char* paths, int token_bytes, int64_t seq_len, int6
     gw += s.windows;
     L->shards.push_back(s);
   }
-  L->my_windows = gw / world;  // equal count per rank (drop_last semantics)
-  if (L->my_windows <= 0) { snprintf(err, errlen, "dataset too small: %lld windows for %d ranks", (long long)gw, world); delete L; return nullptr; }
+  L->total_windows = gw;
+  if (gw < world) { snprintf(err, errlen, "dataset too small: %lld windows for %d ranks", (long long)gw, world); delete L; return nullptr; }
   L->nslots = nslots;
   L->slots.assign(slot_ptrs, slot_ptrs + nslots);
   L->state.assign(nslots, 0);
@@ -199,7 +230,24 @@ void* nd_loader_create(const char* paths, int token_bytes, int64_t seq_len, int6
   return L;
 }
 
-int64_t nd_loader_windows_per_rank(void* h) { return static_cast<Loader*>(h)->my_windows; }
+// windows this rank reads per epoch of the global stream (floor; one rank may read one more)
+int64_t nd_loader_windows_per_rank(void* h) {
+  auto* L = static_cast<Loader*>(h);
+  return L->total_windows / L->world;
+}
+
+int64_t nd_loader_total_windows(void* h) { return static_cast<Loader*>(h)->total_windows; }
+
+// global stream position this rank's cursor counts from, and (setter) restart from `base`, cursor 0
+int64_t nd_loader_base(void* h) { return static_cast<Loader*>(h)->base; }
+
+// which global window this rank's sample `sample` (counted from base) reads (tests, diagnostics)
+int64_t nd_loader_window_of(void* h, int64_t sample) {
+  auto* L = static_cast<Loader*>(h);
+  Perm pc;  // the worker thread owns L->perm
+  int64_t pe = -1;
+  return L->window_of(sample, pc, pe);
+}
 
 // Blocks until the next batch is ready; returns its slot index (caller reads slot buffer, then
 // calls nd_loader_release(slot)).
@@ -227,6 +275,14 @@ int64_t nd_loader_cursor(void* h) { return static_cast<Loader*>(h)->cursor; }
 void nd_loader_seek(void* h, int64_t cursor) {
   auto* L = static_cast<Loader*>(h);
   L->stop_worker();
+  L->cursor = cursor;
+  L->start();
+}
+
+void nd_loader_set_base(void* h, int64_t base, int64_t cursor) {
+  auto* L = static_cast<Loader*>(h);
+  L->stop_worker();
+  L->base = base;
   L->cursor = cursor;
   L->start();
 }

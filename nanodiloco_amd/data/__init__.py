@@ -40,7 +40,14 @@ class _DeviceIter:
     def state_dict(self):
         return self.loader.state_dict()
 
-    def load_state_dict(self, d):
+    def load_state_dict(self, d, resized: bool = False):
+        if resized:
+            # HFBatches: each rank reads a CONTIGUOUS shard of the dataset (split_dataset_by_node, the
+            # reference's sharding); another worker count re-cuts every shard, so no cursor maps onto the
+            # new layout without repeating or skipping examples
+            raise RuntimeError("--elastic-resume with --data hf cannot keep the data stream exact (the contiguous "
+                               "per-rank shards move with the worker count); use --data memmap (pre-tokenised "
+                               "shards, scripts/pretokenize.py), whose global stream resumes exactly on any count")
         self.loader.load_state_dict(d)
 
 

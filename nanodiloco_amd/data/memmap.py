@@ -42,6 +42,14 @@ def runtime_lib():
         L.nd_loader_destroy.restype = None
         L.nd_loader_windows_per_rank.argtypes = [P]
         L.nd_loader_windows_per_rank.restype = I64
+        L.nd_loader_total_windows.argtypes = [P]
+        L.nd_loader_total_windows.restype = I64
+        L.nd_loader_base.argtypes = [P]
+        L.nd_loader_base.restype = I64
+        L.nd_loader_set_base.argtypes = [P, I64, I64]
+        L.nd_loader_set_base.restype = None
+        L.nd_loader_window_of.argtypes = [P, I64]
+        L.nd_loader_window_of.restype = I64
         _rt = L
     return _rt
 
@@ -68,11 +76,20 @@ class MemmapTokens:
                                     rank, world_size, 1 if shuffle else 0, prefetch, arr, err, 512)
         if not self.h:
             raise RuntimeError(f"token loader: {err.value.decode()}")
+        self.world_size = world_size
         self._pending = []
 
     @property
     def windows_per_rank(self) -> int:
         return runtime_lib().nd_loader_windows_per_rank(self.h)
+
+    @property
+    def total_windows(self) -> int:
+        return runtime_lib().nd_loader_total_windows(self.h)
+
+    def window_of(self, sample: int) -> int:
+        """Global window index this rank's sample ``sample`` (counted from the stream base) reads."""
+        return runtime_lib().nd_loader_window_of(self.h, int(sample))
 
     def __iter__(self):
         return self
@@ -102,11 +119,21 @@ class MemmapTokens:
         return {"input_ids": ids, "labels": ids}
 
     def state_dict(self):
-        return {"cursor": runtime_lib().nd_loader_cursor(self.h)}
+        L = runtime_lib()
+        return {"cursor": L.nd_loader_cursor(self.h), "base": L.nd_loader_base(self.h), "world": self.world_size}
 
-    def load_state_dict(self, d):
+    def load_state_dict(self, d, resized: bool = False):
+        """``resized`` (``--elastic-resume`` onto a different number of workers): ``d`` is any worker's state
+        (they advance in lockstep); this rank restarts the global stream at the position the old workers had
+        reached together (base + cursor * old world), so no window is repeated or skipped across the resize."""
         self._drain()
-        runtime_lib().nd_loader_seek(self.h, int(d["cursor"]))
+        L = runtime_lib()
+        cursor, base = int(d.get("cursor", 0)), int(d.get("base", 0))
+        world = int(d.get("world", self.world_size))
+        if resized or world != self.world_size:
+            L.nd_loader_set_base(self.h, base + cursor * world, 0)
+        else:
+            L.nd_loader_set_base(self.h, base, cursor)
 
     def close(self):
         if getattr(self, "h", None):

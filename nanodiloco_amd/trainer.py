@@ -224,7 +224,11 @@ class Trainer:
             ds = st.get("data_state")
             if st.get("resized_from") is not None and e.rank == 0:
                 print(f"[elastic resume] {st['resized_from']} -> {e.world_size} workers", flush=True)
-            if ds:
+            if st.get("resized_from") is not None and self.data_kind in ("memmap", "hf"):
+                # --elastic-resume: the stream restarts where the old workers stopped together (memmap), or
+                # the resume refuses (hf: contiguous shards) -- see utils/checkpoint.load_checkpoint
+                self.data.load_state_dict(st.get("data_state_rank0") or {}, resized=True)
+            elif ds:
                 # a data stream that cannot be restored must fail the resume loudly: silently
                 # restarting it would re-train on the same tokens
                 if not hasattr(self.data, "load_state_dict"):

@@ -48,12 +48,13 @@ def _stage_dir(ckpt_dir: str) -> str:
 
 
 def find_checkpoint(ckpt_dir: Optional[str]) -> Optional[str]:
-    """The newest COMPLETE checkpoint for ``ckpt_dir`` (itself, or ``<dir>.old`` when a save was interrupted
-    between its two renames), a pre-round-5 checkpoint without the marker, or None."""
+    """The newest COMPLETE checkpoint for ``ckpt_dir``: itself; else the staging ``<dir>.tmp`` when a save was
+    interrupted after its COMPLETE marker but before its swap finished (newer than ``<dir>.old``); else
+    ``<dir>.old``; else a pre-round-5 checkpoint without the marker; else None."""
     if not ckpt_dir:
         return None
     d = os.path.normpath(ckpt_dir)
-    for cand in (d, d + ".old"):
+    for cand in (d, _stage_dir(d), d + ".old"):
         if os.path.isfile(os.path.join(cand, COMPLETE)):
             return cand
     if os.path.isfile(os.path.join(d, "trainer_state.json")) and not os.path.exists(_stage_dir(d)):
@@ -62,10 +63,13 @@ def find_checkpoint(ckpt_dir: Optional[str]) -> Optional[str]:
 
 
 def _swap_in(stage: str, final: str) -> None:
+    """Make the complete ``stage`` the checkpoint.  At every instant some complete copy is where
+    :func:`find_checkpoint` looks: ``final`` (or ``stage``, or ``final.old``) -- a leftover ``.old`` is deleted
+    only while a complete ``final`` exists, and with no ``final`` the stage moves in before anything is deleted."""
     old = final + ".old"
-    if os.path.isdir(old):
-        shutil.rmtree(old)
     if os.path.isdir(final):
+        if os.path.isdir(old):
+            shutil.rmtree(old)
         os.replace(final, old)
     os.replace(stage, final)
     shutil.rmtree(old, ignore_errors=True)
@@ -135,6 +139,12 @@ def save_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, step: int, data_
         with open(os.path.join(ckpt_dir, "trainer_state.json"), "w") as f:
             json.dump(state, f, indent=2)
     barrier(env)  # every rank's files are in the staging directory
+    # every tensor above went through a host copy (so every collective it depends on has completed or been
+    # aborted, and a watchdog abort sets the sticky error before it releases the collective): a failed own
+    # RCCL communicator must not leave a COMPLETE checkpoint of partially reduced state behind
+    for comm in (getattr(diloco, "outer_comm", None), getattr(diloco, "inner_comm", None)):
+        if comm is not None:
+            comm.check("the checkpoint is marked complete")
     if r == 0:
         with open(os.path.join(ckpt_dir, COMPLETE), "w") as f:
             json.dump({"step": step, "world_size": env.world_size}, f)
@@ -145,9 +155,12 @@ def save_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, step: int, data_
 def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, elastic: bool = False) -> Dict[str, Any]:
     """``elastic`` (``--elastic-resume``): the number of DiLoCo workers may differ from the checkpoint's (one GPU
     per worker, a checkpoint without a pending overlapped outer step).  The shared outer state (theta_sync,
-    outer momentum, schedule) is exact; worker r keeps its own AdamW state and data stream when the
-    checkpoint has rank r, and a NEW worker starts from rank 0's AdamW state with a fresh data stream -- the
-    "average over the survivors" recovery DiLoCo allows."""
+    outer momentum, schedule) is exact; worker r keeps its own AdamW state when the checkpoint has rank r, and a
+    NEW worker starts from rank 0's AdamW state -- the "average over the survivors" recovery DiLoCo allows
+    (SURVEY.md §5.3).  Data: the memmap stream is global (csrc/runtime/token_loader.cpp), so every worker
+    restarts it where the old workers stopped together (``data_state_rank0``; nothing repeated or skipped);
+    the HF loader's contiguous shards cannot be re-cut exactly and the resume refuses; synthetic workers keep
+    their own random stream (new ones draw a fresh one)."""
     found = find_checkpoint(ckpt_dir)
     if found is None:
         raise FileNotFoundError(f"no complete checkpoint at {ckpt_dir}")
@@ -205,6 +218,14 @@ def load_checkpoint(ckpt_dir: str, model, diloco, env: DistEnv, elastic: bool = 
                 if k.startswith("data."):
                     data_state[k[5:]] = v
     state["data_state"] = data_state
+    if resized:
+        # the data sources whose stream is global (memmap) restart every worker -- survivors and new ones --
+        # at the position the old workers reached together; they advance in lockstep, so rank 0's state says
+        per0 = _load_st(os.path.join(ckpt_dir, "rank0.safetensors"))
+        with open(os.path.join(ckpt_dir, "rank0.json")) as f:
+            scal0 = json.load(f)
+        ds0 = {k[5:]: v for k, v in list(per0.items()) + list(scal0.items()) if k.startswith("data.")}
+        state["data_state_rank0"] = ds0
     state["resized_from"] = old_world if resized else None
     store.sync_shadow()
     return state

@@ -129,7 +129,8 @@ def test_memmap_loader_disjoint_deterministic(tmp_path, runtime_lib):
         rows = torch.cat([next(L)["input_ids"] for _ in range(5)])  # one epoch = 20 windows
         starts = set((rows[:, 0] // T).tolist())
         assert len(starts) == 20
-        assert all(int(s) % 2 == r for s in starts)            # rank-strided windows
+        # the two workers read disjoint halves of the global stream (positions r, r + 2, r + 4, ...)
+        assert starts == {L.window_of(k) for k in range(20)}
         assert torch.equal(rows[:, 1:] - rows[:, :-1], torch.ones_like(rows[:, 1:]))  # contiguous windows
         seen.append(starts)
         L.close()
@@ -145,3 +146,34 @@ def test_memmap_loader_disjoint_deterministic(tmp_path, runtime_lib):
     C.load_state_dict(stt)
     for i in range(3, 7):
         assert torch.equal(next(C)["input_ids"], first[i])
+
+
+def test_memmap_elastic_resume_repeats_and_skips_nothing(tmp_path, runtime_lib):
+    """--elastic-resume on another worker count.  Two workers read 3 batches each of epoch 0, then
+    the job resumes on 3 workers from rank 0's state (every worker, survivor or new, gets the same state):
+    until epoch 0 is done no window is read twice and every window is read once."""
+    from nanodiloco_amd.data.memmap import MemmapTokens, write_token_shard
+    T, B, G = 8, 2, 60
+    write_token_shard(str(tmp_path / "a.bin"), np.arange(G * T) % 30000)
+    paths = [str(tmp_path / "a.bin")]
+
+    def windows(L, n):
+        return [int(w) for w in (torch.cat([next(L)["input_ids"] for _ in range(n)])[:, 0] // T).tolist()]
+
+    old = [MemmapTokens(paths, T, B, rank=r, world_size=2, seed=3) for r in range(2)]
+    read = sum((windows(L, 3) for L in old), [])  # 2 workers x 3 batches x 2 = 12 windows
+    st = old[0].state_dict()
+    assert st == {"cursor": 6, "base": 0, "world": 2}
+    new = [MemmapTokens(paths, T, B, rank=r, world_size=3, seed=3) for r in range(3)]
+    for L in new:
+        L.load_state_dict(st, resized=True)
+        assert L.state_dict() == {"cursor": 0, "base": 12, "world": 3}
+    read += sum((windows(L, 8) for L in new), [])  # 3 x 8 x 2 = 48 more: epoch 0 complete
+    assert len(read) == G and len(set(read)) == G  # nothing repeated, nothing skipped
+    # a normal (same-count) resume of a resized stream continues it exactly
+    nxt = windows(new[1], 2)
+    again = MemmapTokens(paths, T, B, rank=1, world_size=3, seed=3)
+    again.load_state_dict({"cursor": 16, "base": 12, "world": 3})
+    assert windows(again, 2) == nxt
+    for L in old + new + [again]:
+        L.close()

@@ -8,13 +8,13 @@ import sys
 import pytest
 import torch
 
-from ._mp import free_port
+from ._mp import child_env, free_port
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _torchrun(nproc, args, tmp_path, timeout=600):
-    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    env = child_env(OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m", "nanodiloco_amd"] + args
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
@@ -95,7 +95,7 @@ def test_resume_matches_uninterrupted(tmp_path, nproc, inner_dp, overlap):
 
 
 def _torchrun_raw(nproc, args, tmp_path, extra_env=None, run_args=(), timeout=600):
-    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT, **(extra_env or {}))
+    env = child_env(OMP_NUM_THREADS="1", **(extra_env or {}))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), *run_args, "-m", "nanodiloco_amd"] + args
     return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
@@ -178,6 +178,16 @@ def test_find_checkpoint_prefers_complete(tmp_path):
     (tmp_path / "ck.old").mkdir()
     (tmp_path / "ck.old" / COMPLETE).write_text('{"step": 4}')
     assert find_checkpoint(str(d)) == str(tmp_path / "ck.old")  # interrupted between the two renames
+    (tmp_path / "ck.tmp" / COMPLETE).write_text('{"step": 5}')
+    assert find_checkpoint(str(d)) == str(tmp_path / "ck.tmp")  # marked complete, swap not begun: newest
+    # resumed from ck.old (no ck), the next save's swap must never leave only the staging copy
+    # unconsidered -- with no final directory the stage moves in BEFORE the old copy is deleted
+    from nanodiloco_amd.utils.checkpoint import _swap_in
+    _swap_in(str(tmp_path / "ck.tmp"), str(d))
+    assert find_checkpoint(str(d)) == str(d) and not (tmp_path / "ck.old").exists()
+    assert (d / COMPLETE).read_text() == '{"step": 5}'
+    import shutil
+    shutil.rmtree(d)
     d.mkdir()
     (d / COMPLETE).write_text('{"step": 6}')
     assert find_checkpoint(str(d)) == str(d)
@@ -197,7 +207,7 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
 
 @pytest.mark.slow
 def test_bench_contract_single_process():
-    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
+    env = child_env(OMP_NUM_THREADS="2")
     r = subprocess.run([sys.executable] + BENCH + ["--gpus", "1"], cwd=ROOT, env=env, capture_output=True,
                        text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -212,7 +222,7 @@ def test_bench_contract_single_process():
 
 @pytest.mark.slow
 def test_bench_contract_two_ranks_gloo():
-    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    env = child_env(OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port())] + BENCH + ["--gpus", "2"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
