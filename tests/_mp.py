@@ -6,6 +6,19 @@ import traceback
 import torch.multiprocessing as mp
 
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child_env(**kw):
+    """Environment of a test's child process: the repo first on PYTHONPATH, the parent's entries KEPT after
+    it (appended, not replaced -- a harness that injects its own path entries, e.g. to observe which native
+    libraries the children load, must still see them), plus ``kw``."""
+    pp = os.environ.get("PYTHONPATH", "")
+    env = dict(os.environ, PYTHONPATH=ROOT + (os.pathsep + pp if pp else ""))
+    env.update({k: str(v) for k, v in kw.items()})
+    return env
+
+
 def free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

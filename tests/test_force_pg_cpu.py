@@ -4,11 +4,13 @@ import os
 import subprocess
 import sys
 
+from ._mp import child_env
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_force_pg_one_rank_gloo_cpu():
-    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="")
+    env = child_env(OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="")
     env.pop("MASTER_ADDR", None)
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "_rccl_check.py"), "gloo"], cwd=ROOT,
                        env=env, capture_output=True, text=True, timeout=600)

@@ -15,7 +15,7 @@ import sys
 import pytest
 import torch
 
-from ._mp import free_port
+from ._mp import child_env, free_port
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -28,7 +28,7 @@ def _gpu(hip_lib):
 
 
 def test_bench_two_ranks_share_gpu_gloo():
-    env = dict(os.environ, OMP_NUM_THREADS="4", PYTHONPATH=ROOT)
+    env = child_env(OMP_NUM_THREADS="4")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--backend", "gloo",
            "--model", "llama_tiny.json", "--batch-size", "16", "--micro-batch", "8", "--seq-len", "256",
@@ -50,7 +50,7 @@ def test_trainer_two_workers_share_gpu_overlap_bf16_comm(tmp_path):
     pseudo-gradient transport and debug replica checks (the outer all-reduce result must be
     bit-identical on both workers), plus a checkpoint that HF-style tooling can read."""
     import os as _os
-    env = dict(os.environ, OMP_NUM_THREADS="4", PYTHONPATH=ROOT)
+    env = child_env(OMP_NUM_THREADS="4")
     log = tmp_path / "log.jsonl"
     ck = tmp_path / "ckpt"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
@@ -75,7 +75,7 @@ def test_crash_restart_resume_auto_rccl_one_gpu(tmp_path):
     (parallel/dist.py) and ``--resume auto`` continues from the step-2 checkpoint to the end."""
     ck = tmp_path / "ck"
     log = tmp_path / "m.jsonl"
-    env = dict(os.environ, OMP_NUM_THREADS="4", PYTHONPATH=ROOT, ND_FAULT_INJECT="0:3")
+    env = child_env(OMP_NUM_THREADS="4", ND_FAULT_INJECT="0:3")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), "--max-restarts", "1", "-m", "nanodiloco_amd",
            "--llama-config-file", "configs/llama_tiny.json", "--batch-size", "8", "--per-device-batch-size", "4",

@@ -12,6 +12,8 @@ import sys
 
 import pytest
 
+from ._mp import child_env
+
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -56,7 +58,7 @@ print(json.dumps({"losses": losses, "sum": float(m.store.master.double().sum().i
 
 
 def _run(extra_env, out):
-    env = dict(os.environ, PYTHONPATH=ROOT, ND_RACE_OUT=str(out), **extra_env)
+    env = child_env(ND_RACE_OUT=str(out), **extra_env)
     r = subprocess.run([sys.executable, "-c", SCRIPT], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
