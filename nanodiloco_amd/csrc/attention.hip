@@ -225,6 +225,82 @@ __device__ __forceinline__ float pair_sum32(float x) {
 // here are <= 0 (scores minus a running max / LSE); results below 2^-126 flush to 0, harmless for P.
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Softmax-arithmetic experiment switches, compiled into A/B side libraries only
+// (`build.py --rev ... --extra-flags -DND_ATTN_X=<bits>`); the product library is built with 0.
+//   1  s_setprio 1 around the S (/ dP) MFMA chains, the critical path of every kernel
+//   2  packed f32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32) for the score transform, the row sum and
+//      the dS products -- bitwise the scalar forms (same per-element ops, same summation order)
+//   4  forward: 4 of every 32 exp2s by round-to-nearest range reduction + a degree-6 polynomial on the
+//      FMA pipe instead of v_exp_f32
+//   8  s_setprio 1 around the P V (fwd) / dQ (dq) / dV dK (dkdv) MFMA chains
+//  16  s_setprio 1 around the softmax / dS VALU block instead (the critical path between the two chains)
+//  32  forward: 3 waves / SIMD (launch bound 3, 168 VGPRs, no spill) instead of 4
+#ifndef ND_ATTN_X
+#define ND_ATTN_X 0
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+template <int BIT>
+__device__ __forceinline__ void xprio(int p) {
+  if constexpr ((ND_ATTN_X & BIT) != 0) {
+    if (p) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  }
+}
+// In-kernel segment stamps (diagnostic build only: -DND_ATTN_STAMP, never the product library; guide
+// cdna_hip_programming.md §7 "In-kernel stamps"): s_memtime + lgkmcnt(0) as one statement between scheduling
+// barriers; each segment's cycles are summed in scalar registers and every wave's lane 0 writes its sums to a
+// buffer of its own (nd_attn_stamp_buffer) -- no output value depends on them.  Read SHARES, not run time.
+#ifdef ND_ATTN_STAMP
+__device__ unsigned long long* g_stamp_buf;
+constexpr int kStampSeg = 8;
+struct Stamps {
+  unsigned long long last = 0, sum[kStampSeg] = {0, 0, 0, 0, 0, 0, 0, 0};
+  __device__ __forceinline__ static unsigned long long now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+  }
+  __device__ __forceinline__ void start() { last = now(); }
+  __device__ __forceinline__ void mark(int seg) {
+    const unsigned long long t = now();
+    sum[seg] += t - last;
+    last = t;
+  }
+  __device__ __forceinline__ void flush(int kernel_id) {
+    if ((threadIdx.x & 63) == 0 && g_stamp_buf) {
+      const unsigned long long wid = (unsigned long long)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+      unsigned long long* o = g_stamp_buf + 1 + (wid * kStampSeg) + (unsigned long long)kernel_id * (1ull << 22);
+      for (int k = 0; k < kStampSeg; ++k) o[k] = sum[k];
+    }
+  }
+};
+ND_API int nd_attn_stamp_buffer(void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_buf), &p, sizeof(p));
+}
+#define ND_STAMP(x) x
+#else
+#define ND_STAMP(x)
+#endif
+
+// 2^x for x <= 0 without the transcendental unit: x = j + f, j = rint(x) by the 1.5 * 2^23 shifter,
+// f in [-0.5, 0.5], 2^f by its degree-6 Taylor polynomial (relative error < 2e-7), 2^j into the exponent.
+__device__ __forceinline__ float pexp2(float x) {
+  const float xc = fmaxf(x, -126.f);
+  const float t = xc + 12582912.f;
+  const float f = xc - (t - 12582912.f);
+  float p = fmaf(1.5403530e-4f, f, 1.3333558e-3f);
+  p = fmaf(p, f, 9.6181291e-3f);
+  p = fmaf(p, f, 5.5504109e-2f);
+  p = fmaf(p, f, 2.4022651e-1f);
+  p = fmaf(p, f, 6.9314718e-1f);
+  p = fmaf(p, f, 1.f);
+  const float r = __int_as_float(__float_as_int(p) + ((__float_as_int(t) - 0x4B400000) << 23));
+  return x < -126.f ? 0.f : r;
+}
+
 // Store a [HD x 32] transposed accumulator (rows = head dim in registers, col = row index on the
 // lane) as 8-B packed bf16 groups into row `out_row`.  With tables, the inverse RoPE rotation is
 // applied first: head-dim rows d and d + HD/2 sit in the same lane (o <-> o + NO/2, or register
@@ -343,7 +419,7 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
 // LDS-DMA path since the tile loop is unrolled (ND_ATTN_ABL=0 for the plain one).
 // NW: waves per workgroup (4 or 8; 8 = 256-query blocks, every K/V tile DMA'd once per 256 queries: DMA only)
 template <int HD, bool ROPE, bool DMA = false, bool PAD = false, int ABL = 0, int NW = 4>  // DMA: LDS-DMA K/V staging (!ROPE, T % 64 == 0)
-__global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA) ? 4 : 3)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+__global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA && !(ND_ATTN_X & 32)) ? 4 : 3)) attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int nh, int nkv, int T,
                                                           int64_t ld, int64_t ldo, float scale,
@@ -400,6 +476,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA) ? 
     tdma.issue(Kb + (int64_t)j * BN * ld, ks_a + off);
     tdma.issue(Vb + (int64_t)j * BN * ld, vs_a + off);
   };
+  ND_STAMP(Stamps stp; stp.start();)
   if constexpr (DMA) {
     // double-buffered tiles: wait(tile j) + barrier | DMA tile j+1 -> buf (j+1)&1 | compute(buf j&1)
     tdma.init(ld);
@@ -427,9 +504,13 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA) ? 
     const bf16_t* Kt = Ks + PAR * (BN * HD);
     const bf16_t* Vt = Vs + PAR * (BN * HD);
     if constexpr (DMA) {
+      ND_STAMP(stp.mark(7);)
       if constexpr (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ND_STAMP(stp.mark(0);)
       if constexpr (!(ABL & 2)) __syncthreads();
+      ND_STAMP(stp.mark(1);)
       if constexpr (!(ABL & 1)) if (j + 1 < ntiles) dma_issue(j + 1);
+      ND_STAMP(stp.mark(2);)
     }
     if (k0 <= q0w + 31) {  // else: whole tile above this wave's diagonal (wave-uniform)
       // K row fragments issued up front (V^T transposing reads stay next to their MFMAs: holding
@@ -440,6 +521,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA) ? 
 #pragma unroll
         for (int t = 0; t < NT; ++t) ka[kt][t] = row_frag<HD>(Kt, kt * 32 + c32, t, h);
       f32x16 s[2];
+      xprio<1>(1);
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         s[kt] = f32x16{};
@@ -449,6 +531,8 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA) ? 
           else s[kt] = mfma32(ka[kt][t], qf[t], s[kt]);
         }
       }
+      xprio<1>(0);
+      ND_STAMP(stp.mark(3);)
       if constexpr (ABL & 4) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
@@ -463,6 +547,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA) ? 
           }
         return;
       }
+      xprio<16>(1);
       float mx;
       if constexpr (ABL & 32) {
         // variant 32: one compare + select per score against a per-lane limit (T % 64 == 0 here: no
@@ -516,21 +601,48 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA) ? 
       m = mnew;
       float rs4[4] = {0.f, 0.f, 0.f, 0.f};  // variant 32: four independent partial sums
       float rs = 0.f;
+      if constexpr ((ND_ATTN_X & 2) != 0 && (ABL & 32) != 0) {
+        // packed: rsp[0] = (rs4[0], rs4[1]), rsp[1] = (rs4[2], rs4[3]) -- the scalar order exactly
+        f2v rsp[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+        const f2v c2 = {c, c}, nm2 = {-mref, -mref};
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            f2v x = pk_fma(f2v{s[kt][r], s[kt][r + 1]}, c2, nm2);
+            if constexpr ((ND_ATTN_X & 4) != 0) {
+              x.x = fexp2(x.x);
+              x.y = (r & 7) == 6 ? pexp2(x.y) : fexp2(x.y);
+            } else {
+              x.x = fexp2(x.x);
+              x.y = fexp2(x.y);
+            }
+            s[kt][r] = x.x;
+            s[kt][r + 1] = x.y;
+            rsp[(r >> 1) & 1] += x;
+          }
+        rs = (rsp[0].x + rsp[0].y) + (rsp[1].x + rsp[1].y);
+      } else {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = fexp2(fmaf(s[kt][r], c, -mref));
+          const float xx = fmaf(s[kt][r], c, -mref);
+          const float p = ((ND_ATTN_X & 4) != 0 && (r & 7) == 7) ? pexp2(xx) : fexp2(xx);
           s[kt][r] = p;
           if constexpr (ABL & 32) rs4[r & 3] += p;
           else rs += p;
         }
       if constexpr (ABL & 32) rs = (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);
+      }
       l = l * alpha + rs;
       if (__any(alpha != 1.f)) {
 #pragma unroll
         for (int o = 0; o < NO; ++o) oacc[o] *= alpha;
       }
+      xprio<16>(0);
+      ND_STAMP(stp.mark(4);)
+      xprio<8>(1);
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -542,6 +654,8 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA) ? 
             else oacc[o] = mfma32(tr_frag<HD>(Vt, kt * 32 + 16 * sidx, o * 32, g, i16), pf, oacc[o]);
           }
         }
+      xprio<8>(0);
+      ND_STAMP(stp.mark(5);)
     }
     if constexpr (!DMA) {
       if (j + 1 < ntiles) {
@@ -563,12 +677,14 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA) ? 
   } else {
     for (int j = 0; j < ntiles; ++j) tile(j, j & 1);
   }
+  ND_STAMP(stp.mark(7);)
   const float lt = pair_sum32(l);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   if (qi < T) {
     store_T<HD>(O + ((int64_t)b * T + qi) * ldo + (int64_t)head * HD, oacc, inv, h, nullptr, nullptr, 0);
     if (h == 0) LSE[((int64_t)b * nh + head) * T + qi] = m + log2f(lt);
   }
+  ND_STAMP(stp.mark(6); stp.flush(0);)
 }
 
 // =============================================================================== backward
@@ -730,14 +846,30 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kern
 #pragma unroll
           for (int o = 0; o < NO; ++o) tk[sidx][o] = tr_frag<HD>(Kt, kt * 32 + 16 * sidx, o * 32, g, i16);
         f32x16 s = f32x16{}, dp = f32x16{};
+        xprio<1>(1);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           s = mfma32(ka[t], qf[t], s);
           dp = mfma32(va[t], dof[t], dp);
         }
+        xprio<1>(0);
+        xprio<16>(1);
         if (!diag) {
+          if constexpr ((ND_ATTN_X & 2) != 0) {
+            const f2v c2 = {c, c}, nl2 = {-lse, -lse}, nd2 = {-dlt, -dlt};
 #pragma unroll
-          for (int r = 0; r < 16; ++r) dp[r] = fexp2(fmaf(s[r], c, -lse)) * (dp[r] - dlt);
+            for (int r = 0; r < 16; r += 2) {
+              f2v x = pk_fma(f2v{s[r], s[r + 1]}, c2, nl2);
+              x.x = fexp2(x.x);
+              x.y = fexp2(x.y);
+              const f2v y = x * (f2v{dp[r], dp[r + 1]} + nd2);
+              dp[r] = y.x;
+              dp[r + 1] = y.y;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dp[r] = fexp2(fmaf(s[r], c, -lse)) * (dp[r] - dlt);
+          }
         } else {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -746,12 +878,15 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kern
             dp[r] = p * (dp[r] - dlt);
           }
         }
+        xprio<16>(0);
+        xprio<8>(1);
 #pragma unroll
         for (int sidx = 0; sidx < 2; ++sidx) {
           const bf16x8 dsf = pack_frag(dp, sidx);
 #pragma unroll
           for (int o = 0; o < NO; ++o) dq[o] = mfma32(tk[sidx][o], dsf, dq[o]);
         }
+        xprio<8>(0);
       }
     }
     if constexpr (!DMA) {
@@ -1182,7 +1317,9 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
     if (j < nit) issue(j);
   bf16x8 qa[NT], da[NT], tdo[2][NO], tq[2][NO];
   bool first = true;
+  ND_STAMP(Stamps stp; stp.start();)
   for (int it = 0; it < nit; ++it) {
+    ND_STAMP(stp.mark(7);)
     if constexpr (!(ABL & 1)) {  // this wave's part of tile it has landed; tiles it+1 .. it+NB-2 may stay in flight
       if constexpr (NB > 2) {
         constexpr int PT = 2 * IPW;  // per tile and wave, plus 2 statistics loads on waves < BQ / 64
@@ -1196,7 +1333,9 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
         dkdv_vm<0>();
       }
     }
+    ND_STAMP(stp.mark(0);)
     if constexpr (!(ABL & 2)) __syncthreads();        // everyone's; and tile it-1's buffer is free
+    ND_STAMP(stp.mark(1);)
     if constexpr (!(ABL & 1)) if (it + NB - 1 < nit) issue(it + NB - 1);
     const int q0 = qstart + (it % ntq) * BQ;
     const int buf = it % NB;
@@ -1211,6 +1350,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
       // All LDS fragments of this step are issued up front (row reads for S / dP, transposing reads
       // for dV / dK) so their latency hides behind the MFMA chains and the softmax VALU instead of
       // being exposed one s_waitcnt at a time.
+      ND_STAMP(stp.mark(7);)
       const bool rd = !(ABL & 32) || first;
       first = false;
       if (rd) {
@@ -1238,6 +1378,8 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
             tq[sidx][o] = tr_frag<HD>(Qt, qs * 32 + 16 * sidx, o * 32, g, i16);
           }
       }
+      ND_STAMP(stp.mark(2);)
+      xprio<1>(1);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         if constexpr ((ABL & 8) != 0) {
@@ -1248,14 +1390,32 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
           dp = mfma32(da[t], vf[t], dp);
         }
       }
+      xprio<1>(0);
+      ND_STAMP(stp.mark(3);)
+      xprio<16>(1);
       const bool diag = (kw0 + 31 > qsub) || (qsub + 31 >= T) || (key >= T) || (PAD && kw0 < ks);
       if constexpr ((ABL & 4) != 0) {
       } else if (!diag) {
+        if constexpr ((ND_ATTN_X & 2) != 0) {
+          const f2v c2 = {c, c};
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            f2v x = f2v{s[r], s[r + 1]} * c2;
+            x.x = fexp2(x.x);
+            x.y = fexp2(x.y);
+            const f2v y = x * f2v{dp[r], dp[r + 1]};
+            s[r] = x.x;
+            s[r + 1] = x.y;
+            dp[r] = y.x;
+            dp[r + 1] = y.y;
+          }
+        } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float p = fexp2(s[r] * c);
           s[r] = p;
           dp[r] = p * dp[r];
+        }
         }
       } else {
 #pragma unroll
@@ -1266,6 +1426,9 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
           dp[r] = p * dp[r];
         }
       }
+      xprio<16>(0);
+      ND_STAMP(stp.mark(4);)
+      xprio<8>(1);
 #pragma unroll
       for (int sidx = 0; sidx < 2; ++sidx) {
         const bf16x8 pf = pack_frag(s, sidx);
@@ -1281,13 +1444,17 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
           }
         }
       }
+      xprio<8>(0);
+      ND_STAMP(stp.mark(5);)
     }
   }
+  ND_STAMP(stp.mark(7);)
   if constexpr ((ABL & 1) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (key < T) {
     store_T<HD>(dK + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dk, scale, h, ROPE_OUT ? cosT : nullptr, sinT, key);
     store_T<HD>(dV + ((int64_t)b * T + key) * ld + (int64_t)kvh * HD, dv, 1.f, h, nullptr, nullptr, 0);
   }
+  ND_STAMP(stp.mark(6); stp.flush(1);)
 }
 
 template <int HD, bool ROPE, bool ROPE_OUT, bool PAD>

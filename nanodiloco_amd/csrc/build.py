@@ -228,7 +228,9 @@ def main(argv=None):
         print(build_ablation(a.jobs))
         return
     if a.rev:
-        print(build_revision(a.rev, a.jobs, a.extra_flags.split(), not a.no_file_flags, a.tag))
+        # --rev WT: the working tree (uncommitted edits) into _lib/alt/libnd_kernels_<tag>.so
+        rev = None if a.rev == "WT" else a.rev
+        print(build_revision(rev, a.jobs, a.extra_flags.split(), not a.no_file_flags, a.tag))
         return
     out = build(force=a.force, jobs=a.jobs, save_temps=a.save_temps, verbose=True)
     print(out)

@@ -35,6 +35,9 @@ def timed(fn, iters):
     return s.elapsed_time(e) / iters * 1e3  # us
 
 
+OUTPUTS = {}  # workload -> tensors it writes (bitwise comparison of the two libraries, --what attnk)
+
+
 def workloads(what):
     from nanodiloco_amd.ops.attention import rope_cache
     out = {}
@@ -91,6 +94,8 @@ def workloads(what):
         fwd()
         out["attn_fwd"] = fwd
         out["attn_bwd"] = bwd
+        OUTPUTS["attn_fwd"] = (o, lse)
+        OUTPUTS["attn_bwd"] = (dqkv,)
     elif what == "epi":  # the fused-epilogue ping-pong GEMMs at the Llama-150M bench shapes
         from nanodiloco_amd.ops import gemm as G
         M, d, F = 131072, 1024, 2688
@@ -137,7 +142,17 @@ def main():
                 res[k]["alt"].append(timed(fn, a.iters))
     for k, r in res.items():
         n, o = min(r["new"]), min(r["alt"])
-        print(f"{k:10s} working-tree {n:9.1f} us | alt {o:9.1f} us | speedup {o / n:5.3f}x", flush=True)
+        same = ""
+        if k in OUTPUTS:
+            wl[k]()
+            mine = [t.clone() for t in OUTPUTS[k]]
+            with _ext.using(alt):
+                wl[k]()
+            torch.cuda.synchronize()
+            same = " | bitwise " + ("equal" if all(torch.equal(a, b) for a, b in zip(mine, OUTPUTS[k])) else
+                                    "DIFFERENT (max %.3g)" % max((a.float() - b.float()).abs().max().item()
+                                                                 for a, b in zip(mine, OUTPUTS[k])))
+        print(f"{k:10s} working-tree {n:9.1f} us | alt {o:9.1f} us | speedup {o / n:5.3f}x{same}", flush=True)
     del base
 
 
