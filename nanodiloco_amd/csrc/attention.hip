@@ -235,6 +235,10 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 //   8  s_setprio 1 around the P V (fwd) / dQ (dq) / dV dK (dkdv) MFMA chains
 //  16  s_setprio 1 around the softmax / dS VALU block instead (the critical path between the two chains)
 //  32  forward: 3 waves / SIMD (launch bound 3, 168 VGPRs, no spill) instead of 4
+//  64  dK/dV: 64-query tiles at 3 waves / SIMD (launch bound 3: 33 KiB of LDS, <= 168 VGPRs) instead of
+//      128-query tiles at 2
+// 128  dK/dV (128-query tiles): the next tile's LDS-DMA pieces spread over the first three 32-query steps (Q, then
+//      dO, then the row statistics) instead of all issued after the tile's barrier
 #ifndef ND_ATTN_X
 #define ND_ATTN_X 0
 #endif
@@ -253,9 +257,9 @@ __device__ __forceinline__ void xprio(int p) {
 // buffer of its own (nd_attn_stamp_buffer) -- no output value depends on them.  Read SHARES, not run time.
 #ifdef ND_ATTN_STAMP
 __device__ unsigned long long* g_stamp_buf;
-constexpr int kStampSeg = 8;
+constexpr int kStampSeg = 10;
 struct Stamps {
-  unsigned long long last = 0, sum[kStampSeg] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long last = 0, sum[kStampSeg] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   __device__ __forceinline__ static unsigned long long now() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
@@ -1234,7 +1238,7 @@ template <int N> __device__ __forceinline__ void dkdv_vm() { asm volatile("s_wai
 
 // NB: Q / dO / statistics buffers in LDS; tile it + NB - 1 is in flight while tile it is computed
 template <int HD, bool ROPE_OUT, int BQ = 64, bool PAD = false, int NW = 4, int ABL = 0, int NB = 2>
-__global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dma_kernel(
+__global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && BQ == 64 && (ND_ATTN_X & 64)) ? 3 : 2)) attn_bwd_dkdv_dma_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ NL, const float* __restrict__ ND, bf16_t* __restrict__ dK,
     bf16_t* __restrict__ dV, int B, int nh, int nkv, int T, int64_t ld, int64_t ldo, float scale,
@@ -1294,7 +1298,9 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
   const int qstart = (kb * KB) / BQ * BQ;
   const int ntq = (T - qstart + BQ - 1) / BQ;
   const int nit = ntq * rep;
-  auto issue = [&](int it) {
+  ND_STAMP(Stamps stp; stp.start();)
+  // part: 7 = everything; 1 = Q pieces, 2 = dO pieces, 4 = row statistics (ND_ATTN_X & 128 spreads them)
+  auto issue = [&](int it, int part = 7) {
     const int head = kvh * rep + it / ntq;
     const int q0 = qstart + (it % ntq) * BQ;
     const int buf = it % NB;
@@ -1303,21 +1309,23 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
       const uint32_t off = (uint32_t)(buf * BQ * HD * 2 + (wu + NW * i) * 1024);
-      adma_b128(sq, vq[i], qs_a + off);
-      adma_b128(sd, vd[i], do_a + off);
+      if (part & 1) adma_b128(sq, vq[i], qs_a + off);
+      if (part & 2) adma_b128(sd, vd[i], do_a + off);
     }
-    if (wu < BQ / 64) {  // one 64-float wave-instruction per 64 rows
+    ND_STAMP(stp.mark(9);)
+    if ((part & 4) && wu < BQ / 64) {  // one 64-float wave-instruction per 64 rows
       const int64_t rs = ((int64_t)b * nh + head) * T + q0 + wu * 64;
       adma_b32(NL + rs, (uint32_t)(lane * 4), ls_a + (buf * BQ + wu * 64) * 4);
       adma_b32(ND + rs, (uint32_t)(lane * 4), ds_a + (buf * BQ + wu * 64) * 4);
     }
+    ND_STAMP(stp.mark(8);)
   };
 #pragma unroll
   for (int j = 0; j < NB - 1; ++j)
     if (j < nit) issue(j);
   bf16x8 qa[NT], da[NT], tdo[2][NO], tq[2][NO];
   bool first = true;
-  ND_STAMP(Stamps stp; stp.start();)
+  constexpr bool SPREAD = (ND_ATTN_X & 128) != 0 && BQ == 128 && NB == 2;
   for (int it = 0; it < nit; ++it) {
     ND_STAMP(stp.mark(7);)
     if constexpr (!(ABL & 1)) {  // this wave's part of tile it has landed; tiles it+1 .. it+NB-2 may stay in flight
@@ -1336,7 +1344,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
     ND_STAMP(stp.mark(0);)
     if constexpr (!(ABL & 2)) __syncthreads();        // everyone's; and tile it-1's buffer is free
     ND_STAMP(stp.mark(1);)
-    if constexpr (!(ABL & 1)) if (it + NB - 1 < nit) issue(it + NB - 1);
+    if constexpr (!(ABL & 1) && !SPREAD) if (it + NB - 1 < nit) issue(it + NB - 1);
     const int q0 = qstart + (it % ntq) * BQ;
     const int buf = it % NB;
     const bf16_t* Qt = Qs + buf * (BQ * HD);
@@ -1345,13 +1353,18 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
     const float* dt = del_s + buf * BQ;
 #pragma unroll
     for (int qs = 0; qs < BQ / 32; ++qs) {
+      if constexpr (SPREAD && !(ABL & 1))
+        if (qs < 3 && it + 1 < nit) issue(it + 1, 1 << qs);  // before the skip test: every wave issues its pieces
       const int qsub = q0 + qs * 32;
       if (kw0 > qsub + 31 || kw0 >= T) continue;  // wave-uniform: no query >= any of our keys
       // All LDS fragments of this step are issued up front (row reads for S / dP, transposing reads
       // for dV / dK) so their latency hides behind the MFMA chains and the softmax VALU instead of
       // being exposed one s_waitcnt at a time.
       ND_STAMP(stp.mark(7);)
-      const bool rd = !(ABL & 32) || first;
+      // ND_ATTN_X & 64 (A/B): fragments read just before their MFMAs instead, in three phases the scheduler
+      // may not merge -- the register budget of 3 waves / SIMD; the partner waves cover the read latency
+      constexpr bool JIT = (ND_ATTN_X & 64) != 0 && HD == 64 && BQ == 64;
+      const bool rd = (!(ABL & 32) || first) && !JIT;
       first = false;
       if (rd) {
 #pragma unroll
@@ -1385,11 +1398,15 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
         if constexpr ((ABL & 8) != 0) {
           s[t] += (float)qa[t][0];
           dp[t] += (float)da[t][0];
+        } else if constexpr (JIT) {
+          s = mfma32(row_frag<HD>(Qt, qs * 32 + c32, t, h), kf[t], s);
+          dp = mfma32(row_frag<HD>(dOt, qs * 32 + c32, t, h), vf[t], dp);
         } else {
           s = mfma32(qa[t], kf[t], s);
           dp = mfma32(da[t], vf[t], dp);
         }
       }
+      if constexpr (JIT) __builtin_amdgcn_sched_barrier(0);
       xprio<1>(0);
       ND_STAMP(stp.mark(3);)
       xprio<16>(1);
@@ -1427,6 +1444,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
         }
       }
       xprio<16>(0);
+      if constexpr (JIT) __builtin_amdgcn_sched_barrier(0);
       ND_STAMP(stp.mark(4);)
       xprio<8>(1);
 #pragma unroll
@@ -1438,6 +1456,9 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_dm
           if constexpr ((ABL & 16) != 0) {
             dv[o][sidx] += (float)pf[o] + (float)tdo[sidx][o][0];
             dk[o][sidx] += (float)dsf[o] + (float)tq[sidx][o][0];
+          } else if constexpr (JIT) {
+            dv[o] = mfma32(tr_frag<HD>(dOt, qs * 32 + 16 * sidx, o * 32, g, i16), pf, dv[o]);
+            dk[o] = mfma32(tr_frag<HD>(Qt, qs * 32 + 16 * sidx, o * 32, g, i16), dsf, dk[o]);
           } else {
             dv[o] = mfma32(tdo[sidx][o], pf, dv[o]);
             dk[o] = mfma32(tq[sidx][o], dsf, dk[o]);
@@ -1569,7 +1590,7 @@ static int bwd_fused_launch(const void* q, const void* k, const void* v, const v
     else if (nbv == 3) ND_DN(3);
     else ND_DN(4);
 #undef ND_DN
-  } else if (T % 128 == 0) {
+  } else if (T % 128 == 0 && !(ND_ATTN_X & 64)) {
     switch (g_attn.dkdv_abl) {  // always 0 outside an ND_ABLATION build
 #ifdef ND_ABLATION
 #define ND_DA(X) case X: hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<HD, ROPE_OUT, 128, PAD, 4, X>), dim3(nb * B * nkv), \

@@ -20,10 +20,11 @@ from nanodiloco_amd.ops import _ext  # noqa: E402
 SEGS = {
     0: {0: "wait K/V LDS-DMA (vmcnt)", 1: "barrier", 2: "issue next K/V DMA", 3: "K reads + S MFMAs (issue)",
         4: "mask / max / exp / row sum (VALU, waits S)", 5: "P pack + V^T reads + P V MFMAs (issue)",
-        6: "epilogue (O / LSE store)", 7: "loop overhead / skipped tiles"},
+        6: "epilogue (O / LSE store)", 7: "loop overhead / skipped tiles", 8: "-", 9: "-"},
     1: {0: "wait Q/dO/stat LDS-DMA (vmcnt)", 1: "barrier", 2: "LDS fragment + seed reads (to landed)",
         3: "S / dP MFMAs (issue)", 4: "exp / P*dP (VALU, waits S, dP)", 5: "pack + dV / dK MFMAs (issue)",
-        6: "epilogue (dK / dV store)", 7: "DMA issue / loop overhead / skipped steps"},
+        6: "epilogue (dK / dV store)", 7: "loop overhead / skipped steps", 8: "issue row-statistic LDS-DMA pieces",
+        9: "issue Q / dO LDS-DMA pieces"},
 }
 
 ap = argparse.ArgumentParser()
@@ -65,11 +66,11 @@ torch.cuda.synchronize()
 _ext.check(raw.nd_attn_stamp_buffer(ctypes.c_void_p(0)), "stamp buffer")
 h = buf.cpu()
 for kid, name in ((0, "attn_fwd_kernel"), (1, "attn_bwd_dkdv_dma_kernel")):
-    seg = h[1 + kid * (1 << 22): 1 + kid * (1 << 22) + (1 << 22) - 8].view(-1, 8)
+    seg = h[1 + kid * (1 << 22): 1 + kid * (1 << 22) + (1 << 22) // 10 * 10].view(-1, 10)
     seg = seg[seg.sum(1) > 0].double()
     tot = seg.sum(0)
     allc = tot.sum().item()
     print(f"{name}: {seg.shape[0]} waves, {allc / seg.shape[0]:.0f} stamped cycles per wave (mean)")
-    for s_ in range(8):
+    for s_ in range(10):
         print(f"  {s_}  {SEGS[kid][s_]:48s} {100 * tot[s_].item() / allc:5.1f} %   "
               f"{tot[s_].item() / seg.shape[0]:9.0f} cyc/wave")
