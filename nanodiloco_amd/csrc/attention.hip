@@ -239,6 +239,8 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 //      128-query tiles at 2
 // 128  dK/dV (128-query tiles): the next tile's LDS-DMA pieces spread over the first three 32-query steps (Q, then
 //      dO, then the row statistics) instead of all issued after the tile's barrier
+// 256  forward: the two 32-key S chains interleaved MFMA by MFMA instead of one after the other
+// 512  the round-5 wait placement (no settle() of the prologue fragment loads; A/B of the fix only)
 #ifndef ND_ATTN_X
 #define ND_ATTN_X 0
 #endif
@@ -288,6 +290,21 @@ ND_API int nd_attn_stamp_buffer(void* p) {
 #else
 #define ND_STAMP(x)
 #endif
+
+// Retire the prologue's fragment loads (Q / dO in the forward and dQ kernels, K / V in dK/dV) BEFORE the tile
+// loop.  Left alone, the compiler's wait-count pass keeps them "possibly outstanding" at the loop header (the
+// loop body does not always use them: causally skipped tiles) and puts an s_waitcnt vmcnt(N) in front of their
+// first use in EVERY iteration; the hardware counter also holds the LDS-DMA pieces the iteration has just issued
+// (inline asm, invisible to the pass), so that wait stalled each tile / step until most of its prefetch had
+// landed -- a full memory round trip per iteration.  An empty asm that consumes the registers makes the pass put
+// one vmcnt(0) here instead.
+template <int N>
+__device__ __forceinline__ void settle(const bf16x8 (&f)[N]) {
+  if constexpr ((ND_ATTN_X & 512) == 0) {
+#pragma unroll
+    for (int t = 0; t < N; ++t) asm volatile("" ::"v"(f[t]));
+  }
+}
 
 // 2^x for x <= 0 without the transcendental unit: x = j + f, j = rint(x) by the 1.5 * 2^23 shifter,
 // f in [-0.5, 0.5], 2^f by its degree-6 Taylor polynomial (relative error < 2e-7), 2^j into the exponent.
@@ -465,6 +482,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA && 
 #pragma unroll
   for (int t = 0; t < NT; ++t) qf[t] = qi < T ? load16(Qb + (int64_t)qi * ld + 16 * t + 8 * h) : zero8();
   if (ROPE && qi < T) rope_frags<HD>(qf, cosT, sinT, qi, h);
+  settle(qf);
   f32x16 oacc[NO];
 #pragma unroll
   for (int o = 0; o < NO; ++o) oacc[o] = f32x16{};
@@ -526,6 +544,15 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA && 
         for (int t = 0; t < NT; ++t) ka[kt][t] = row_frag<HD>(Kt, kt * 32 + c32, t, h);
       f32x16 s[2];
       xprio<1>(1);
+      if constexpr ((ND_ATTN_X & 256) != 0 && !(ABL & 16)) {
+        // the two 32-key chains interleaved: two MFMAs between a K-fragment read and its use, not one
+        s[0] = f32x16{};
+        s[1] = f32x16{};
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) s[kt] = mfma32(ka[kt][t], qf[t], s[kt]);
+      } else {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         s[kt] = f32x16{};
@@ -534,6 +561,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && DMA && 
           if constexpr (ABL & 16) s[kt][t] += (float)ka[kt][t][0];
           else s[kt] = mfma32(ka[kt][t], qf[t], s[kt]);
         }
+      }
       }
       xprio<1>(0);
       ND_STAMP(stp.mark(3);)
@@ -796,6 +824,8 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kern
   } else {
     dlt = qi < T ? DELTA[rowstat + qi] : 0.f;
   }
+  settle(qf);
+  settle(dof);
   f32x16 dq[NO];
 #pragma unroll
   for (int o = 0; o < NO; ++o) dq[o] = f32x16{};
@@ -954,6 +984,8 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
     vf[t] = key < T ? load16(Vb + (int64_t)key * ld + 16 * t + 8 * h) : zero8();
   }
   if (ROPE && key < T) rope_frags<HD>(kf, cosT, sinT, key, h);
+  settle(kf);
+  settle(vf);
   f32x16 dk[NO], dv[NO];
 #pragma unroll
   for (int o = 0; o < NO; ++o) { dk[o] = f32x16{}; dv[o] = f32x16{}; }
@@ -1074,9 +1106,12 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
 // forward's 32) are compiled only into a -DND_ABLATION build (`python -m nanodiloco_amd.csrc.build
 // --ablation` -> _lib/alt/libnd_kernels_ablation.so), so a stray ND_ATTN_*ABL variable cannot change
 // what a training job computes.
+#ifndef ND_ATTN_DKDV_ORDER_DEFAULT
+#define ND_ATTN_DKDV_ORDER_DEFAULT 0
+#endif
 struct AttnEnv {
   int order = 1;        // ND_ATTN_ORDER: grid order (see attn_fwd_kernel)
-  int dkdv_order = 0;   // ND_ATTN_DKDV_ORDER: group the key blocks of one (batch, kv head); +1.8 % slower in-step
+  int dkdv_order = ND_ATTN_DKDV_ORDER_DEFAULT;   // ND_ATTN_DKDV_ORDER: group the key blocks of one (batch, kv head)
   float thr = 8.f;      // ND_ATTN_THR: deferred-max threshold (log2 units; 0 = move the max on every increase)
   bool fwd_reg = false; // ND_ATTN_FWD=r: register-staged forward
   int fwd_var = 32;     // ND_ATTN_ABL: 32 (cheaper mask / v_max3 tree, 1.007-1.024x) or 0 (plain)
@@ -1278,6 +1313,8 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && BQ == 6
     kf[t] = key < T ? load16(Kb + (int64_t)key * ld + 16 * t + 8 * h) : zero8();
     vf[t] = key < T ? load16(Vb + (int64_t)key * ld + 16 * t + 8 * h) : zero8();
   }
+  settle(kf);
+  settle(vf);
   f32x16 dk[NO], dv[NO];
 #pragma unroll
   for (int o = 0; o < NO; ++o) { dk[o] = f32x16{}; dv[o] = f32x16{}; }
