@@ -112,6 +112,17 @@ def workloads(what):
         out["qkv_plain"] = lambda: G.gemm_pp(x, wq)
         out["gu_plain"] = lambda: G.gemm_pp(x, wgu)
         out["down_dgrad_plain"] = lambda: G.gemm_pp(x, wdt)
+    elif what == "cast":  # fp8 quantisation of the attention backward's d(q|k|v) at the Llama-150M bench shape
+        x = torch.randn(131072, 3072, device="cuda").bfloat16()
+        sc = torch.full((1,), 64.0, device="cuda")
+        q8 = torch.empty(x.shape, device="cuda", dtype=torch.uint8)
+        am = torch.zeros(64, device="cuda")
+
+        def cast():
+            _ext.check(_ext.lib().nd_fp8_cast(x.data_ptr(), _ext.dtcode(x), x.numel(), sc.data_ptr(), q8.data_ptr(), 1,
+                                              am.data_ptr(), am.numel(), _ext.stream_ptr()), "cast")
+        out["cast_e5m2"] = cast
+        OUTPUTS["cast_e5m2"] = (q8,)
     elif what == "wgrad":
         from nanodiloco_amd.ops.gemm import wgrad
         for name, (M, N) in {"qkv": (3072, 1024), "o": (1024, 1024), "gate_up": (5376, 1024),
@@ -126,7 +137,7 @@ def workloads(what):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--alt", required=True)
-    ap.add_argument("--what", default="attn", choices=["attn", "attnk", "step", "wgrad", "ce", "epi"])
+    ap.add_argument("--what", default="attn", choices=["attn", "attnk", "step", "wgrad", "ce", "epi", "cast"])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
