@@ -183,6 +183,50 @@ __device__ __forceinline__ void block_amax_commit(float amax, float* amax_out, i
   }
 }
 
+// Four LDS-DMA wave-instructions (64 lanes x 16 B each) from per-lane byte offsets v0..v3 into LDS lds, lds + ST,
+// lds + 2 ST, lds + 3 ST: m0 is saved / restored once per burst and stepped with one s_add per piece (the
+// compiler reserves m0, so every asm that writes it must restore it; SCC is declared clobbered).  The one wait
+// state between an m0 write and the LDS-DMA that reads it is the s_nop.  FLAT-global form (SGPR base, no range
+// check) and buffer form (range-checked V#: lanes past its record count read nothing).
+#ifndef ND_DMA_BURST
+#define ND_DMA_BURST 1
+#endif
+template <uint32_t ST>
+__device__ __forceinline__ void gdma4(const void* base, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %5\n\t"
+      "s_add_u32 m0, m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %5\n\t"
+      "s_add_u32 m0, m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %5\n\t"
+      "s_add_u32 m0, m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %5\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(base), "s"(lds), "i"(ST)
+      : "memory", "scc");
+}
+template <uint32_t ST>
+__device__ __forceinline__ void gdma2(const void* base, uint32_t v0, uint32_t v1, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\t"
+      "s_add_u32 m0, m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(v0), "v"(v1), "s"(base), "s"(lds), "i"(ST)
+      : "memory", "scc");
+}
+template <uint32_t ST>
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3,
+                                     uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %5, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, %7\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %5, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, %7\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %5, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, %7\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %5, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(r), "s"(lds), "i"(ST)
+      : "memory", "scc");
+}
+
 }  // namespace nd
 
 #define ND_LAUNCH_CHECK() return (int)hipGetLastError()

@@ -573,12 +573,20 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
       const bool full = EPI == PP_SWIGLU ? p.n0 + 128 <= N : p.n0 + 128 * h + 128 <= N;
       if (!(ABL & 1024) && full) {
         const char* base = B + ((int64_t)(p.n0 + (EPI == PP_SWIGLU ? 64 : 128) * h) * ldb + (int64_t)p.kt * TKE) * ES;
+        if constexpr (ND_DMA_BURST) {
+          gdma4<4096>(base, voff[0], voff[1], voff[2], voff[3], dst + (uint32_t)h * HALF_B);
+        } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) gdma(base, voff[q], dst + (uint32_t)h * HALF_B + (uint32_t)q * 4096u);
+          for (int q = 0; q < 4; ++q) gdma(base, voff[q], dst + (uint32_t)h * HALF_B + (uint32_t)q * 4096u);
+        }
       } else {
         const auto r = b_rsrc(p.n0, p.kt, h);
+        if constexpr (ND_DMA_BURST) {
+          dma4<4096>(r, voff[0], voff[1], voff[2], voff[3], dst + (uint32_t)h * HALF_B);
+        } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dma(r, voff[q], dst + (uint32_t)h * HALF_B + (uint32_t)q * 4096u);
+          for (int q = 0; q < 4; ++q) dma(r, voff[q], dst + (uint32_t)h * HALF_B + (uint32_t)q * 4096u);
+        }
       }
     }
   };
@@ -587,12 +595,20 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
     const uint32_t dst = lds0 + (uint32_t)(s & 1) * BUF_B + (uint32_t)h * HALF_B + (uint32_t)wn * 1024u;
     if (!(ABL & 1024) && p.m0 + 128 * h + 128 <= M) {
       const char* base = A + ((int64_t)(p.m0 + 128 * h) * lda + (int64_t)p.kt * TKE) * ES;
+      if constexpr (ND_DMA_BURST) {
+        gdma4<4096>(base, voff[0], voff[1], voff[2], voff[3], dst);
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) gdma(base, voff[q], dst + (uint32_t)q * 4096u);
+        for (int q = 0; q < 4; ++q) gdma(base, voff[q], dst + (uint32_t)q * 4096u);
+      }
     } else {
       const auto r = a_rsrc(p.m0, p.kt, h);
+      if constexpr (ND_DMA_BURST) {
+        dma4<4096>(r, voff[0], voff[1], voff[2], voff[3], dst);
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dma(r, voff[q], dst + (uint32_t)q * 4096u);
+        for (int q = 0; q < 4; ++q) dma(r, voff[q], dst + (uint32_t)q * 4096u);
+      }
     }
   };
 

@@ -502,12 +502,20 @@ __global__ void __launch_bounds__(512, 1) wgrad_pp_kernel(WgProb p0, WgProb p1, 
     const uint32_t dst = lds0 + (uint32_t)(kt & 1) * WPP_BUF_B + (uint32_t)(g == 0 ? 2 + h : h) * WPP_HALF_B +
                          (uint32_t)wn * 1024u;
     if (GD && (g == 0 ? n0 + 128 * h + 128 <= N : m0 + 128 * h + 128 <= M)) {
+      if constexpr (ND_DMA_BURST) {
+        gdma4<4096>((g == 0 ? B : A) + e0, voff[0], voff[1], voff[2], voff[3], dst);
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) wpp_gdma((g == 0 ? B : A) + e0, voff[q], dst + (uint32_t)q * 4096u);
+        for (int q = 0; q < 4; ++q) wpp_gdma((g == 0 ? B : A) + e0, voff[q], dst + (uint32_t)q * 4096u);
+      }
     } else {
       const auto r = wpp_rsrc((g == 0 ? B : A) + e0, ((int64_t)K * ld - e0) * 2);
+      if constexpr (ND_DMA_BURST) {
+        dma4<4096>(r, voff[0], voff[1], voff[2], voff[3], dst);
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) wpp_dma(r, voff[q], dst + (uint32_t)q * 4096u);
+        for (int q = 0; q < 4; ++q) wpp_dma(r, voff[q], dst + (uint32_t)q * 4096u);
+      }
     }
   };
   bf16x8 fa[8][2], fb[4][2];

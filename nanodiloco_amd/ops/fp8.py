@@ -211,6 +211,7 @@ class Fp8Recipe:
         self.fmax = z(capacity)
         self.ready = [False] * capacity
         self.stash: Dict[int, tuple] = {}  # slot -> (grad storage ptr, fp8 copy) from a fused producer
+        self._scr: Optional[torch.Tensor] = None  # first-use amax partials
 
     def new_slot(self, fmt: int) -> int:
         k = self.n
@@ -220,7 +221,12 @@ class Fp8Recipe:
 
     def _first_use(self, x: torch.Tensor, k: int):
         if not self.ready[k]:  # first use: current scaling from this tensor's own amax
-            a = x.detach().abs().amax().float().clamp_min(1e-30)
+            # one amax-only read of x by the own cast kernel (no output), not torch's abs + reduce passes
+            if self._scr is None:
+                self._scr = torch.zeros(AMAX_PARTS, dtype=torch.float32, device=self.device)
+            self._scr.zero_()
+            absmax_into(x.detach(), self._scr)
+            a = self._scr.amax().clamp_min(1e-30)
             s = self.fmax[k] / (a * 2.0 ** self.margin)
             self.scale[k:k + 1].copy_(s.reshape(1))
             self.inv[k:k + 1].copy_((1.0 / s).reshape(1))
