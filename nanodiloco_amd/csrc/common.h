@@ -204,16 +204,6 @@ __device__ __forceinline__ void gdma4(const void* base, uint32_t v0, uint32_t v1
       : "memory", "scc");
 }
 template <uint32_t ST>
-__device__ __forceinline__ void gdma2(const void* base, uint32_t v0, uint32_t v1, uint32_t lds) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\t"
-      "s_add_u32 m0, m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(v0), "v"(v1), "s"(base), "s"(lds), "i"(ST)
-      : "memory", "scc");
-}
-template <uint32_t ST>
 __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3,
                                      uint32_t lds) {
   uint32_t keep;
