@@ -795,6 +795,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kern
   const bf16_t* Kb = K + (int64_t)b * T * ld + (int64_t)kvh * HD;
   const bf16_t* Vb = V + (int64_t)b * T * ld + (int64_t)kvh * HD;
 
+  ND_STAMP(Stamps stp; stp.start();)
   bf16x8 qf[NT], dof[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -854,20 +855,26 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kern
       sv.load(Vb, ld, BN, T);
     }
   }
+  ND_STAMP(stp.mark(9);)
   for (int j = 0; j < ntiles; ++j) {
     const int k0 = j * BN;
     const bf16_t* Kt = Ks + (j & 1) * (BN * HD);
     const bf16_t* Vt = Vs + (j & 1) * (BN * HD);
     if constexpr (DMA) {
+      ND_STAMP(stp.mark(7);)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ND_STAMP(stp.mark(0);)
       __syncthreads();
+      ND_STAMP(stp.mark(1);)
       if (j + 1 < ntiles) dma_issue(j + 1);
+      ND_STAMP(stp.mark(2);)
     }
     if (k0 <= q0w + 31) {
       const bool diag = (k0 + BN - 1 > q0w) || (k0 + BN > T) || (qi >= T) || (PAD && k0 < ks);
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         if (k0 + kt * 32 > q0w + 31) continue;  // this 32-key half is above the wave's diagonal
+        ND_STAMP(stp.mark(7);)
         // fragments issued up front (row reads for S^T / dP^T, transposing reads for dQ)
         bf16x8 ka[NT], va[NT], tk[2][NO];
 #pragma unroll
@@ -879,6 +886,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kern
         for (int sidx = 0; sidx < 2; ++sidx)
 #pragma unroll
           for (int o = 0; o < NO; ++o) tk[sidx][o] = tr_frag<HD>(Kt, kt * 32 + 16 * sidx, o * 32, g, i16);
+        ND_STAMP(stp.mark(3);)
         f32x16 s = f32x16{}, dp = f32x16{};
         xprio<1>(1);
 #pragma unroll
@@ -887,6 +895,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kern
           dp = mfma32(va[t], dof[t], dp);
         }
         xprio<1>(0);
+        ND_STAMP(stp.mark(4);)
         xprio<16>(1);
         if (!diag) {
           if constexpr ((ND_ATTN_X & 2) != 0) {
@@ -913,6 +922,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kern
           }
         }
         xprio<16>(0);
+        ND_STAMP(stp.mark(5);)
         xprio<8>(1);
 #pragma unroll
         for (int sidx = 0; sidx < 2; ++sidx) {
@@ -921,6 +931,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kern
           for (int o = 0; o < NO; ++o) dq[o] = mfma32(tk[sidx][o], dsf, dq[o]);
         }
         xprio<8>(0);
+        ND_STAMP(stp.mark(6);)
       }
     }
     if constexpr (!DMA) {
@@ -935,8 +946,10 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kern
       }
     }
   }
+  ND_STAMP(stp.mark(7);)
   if (qi < T)
     store_T<HD>(dQ + ((int64_t)b * T + qi) * ld + (int64_t)head * HD, dq, scale, h, ROPE_OUT ? cosT : nullptr, sinT, qi);
+  ND_STAMP(stp.mark(8); if (PRE && DMA) stp.flush(2);)
 }
 
 // dK, dV: per 128 keys of one (b, kv head); loops over the GQA group's query heads and 64-query

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Where the attention forward and dK/dV kernels spend a wave's cycles: segment stamps of the diagnostic
+"""Where the attention forward, dK/dV and dQ kernels spend a wave's cycles: segment stamps of the diagnostic
 build (``python -m nanodiloco_amd.csrc.build --rev WT --extra-flags=-DND_ATTN_STAMP --tag stamp``; the product
 library has no stamps).  Runs the Llama-150M bench shape (B=64, T=1024, 16x64, pre-rotated q|k) once per
 kernel and prints each segment's share of the summed wave cycles (guide cdna_hip_programming.md §7: read
@@ -25,6 +25,9 @@ SEGS = {
         3: "S / dP MFMAs (issue)", 4: "exp / P*dP (VALU, waits S, dP)", 5: "pack + dV / dK MFMAs (issue)",
         6: "epilogue (dK / dV store)", 7: "loop overhead / skipped steps", 8: "issue row-statistic LDS-DMA pieces",
         9: "issue Q / dO LDS-DMA pieces"},
+    2: {0: "wait K/V LDS-DMA (vmcnt)", 1: "barrier", 2: "issue next K/V DMA", 3: "K / V / K^T fragment reads (to landed)",
+        4: "S / dP MFMAs (issue)", 5: "exp / dS (VALU, waits S, dP)", 6: "pack + dQ MFMAs (issue)",
+        7: "loop overhead / skipped halves", 8: "epilogue (dQ store)", 9: "prologue (Q / dO loads, row statistics)"},
 }
 
 ap = argparse.ArgumentParser()
@@ -44,7 +47,7 @@ do = torch.randn(B * T, nh * hd, device="cuda").bfloat16()
 dqkv = torch.empty_like(qkv)
 ws = torch.empty(2, B, nh, T, device="cuda")
 st = _ext.stream_ptr(qkv.device)
-buf = torch.zeros(2 * (1 << 22) + 8, dtype=torch.int64, device="cuda")
+buf = torch.zeros(3 * (1 << 22) + 8, dtype=torch.int64, device="cuda")
 
 
 def run():
@@ -65,7 +68,7 @@ run()
 torch.cuda.synchronize()
 _ext.check(raw.nd_attn_stamp_buffer(ctypes.c_void_p(0)), "stamp buffer")
 h = buf.cpu()
-for kid, name in ((0, "attn_fwd_kernel"), (1, "attn_bwd_dkdv_dma_kernel")):
+for kid, name in ((0, "attn_fwd_kernel"), (1, "attn_bwd_dkdv_dma_kernel"), (2, "attn_bwd_dq_kernel")):
     seg = h[1 + kid * (1 << 22): 1 + kid * (1 << 22) + (1 << 22) // 10 * 10].view(-1, 10)
     seg = seg[seg.sum(1) > 0].double()
     tot = seg.sum(0)
