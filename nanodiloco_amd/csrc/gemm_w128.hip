@@ -114,7 +114,13 @@ __host__ __device__ constexpr int nst_tail() {
 // ABL: ablation builds for profiling only (WRONG results): 1 no LDS-DMA in the phases, 2 no fragment
 // reads in the phases, 4 no barriers in the phases, 8 no epilogue stores, 16 no vmcnt waits in the loop;
 // 4096: the loop's pieces as FLAT-global LDS loads (no range check: exact-multiple shapes only)
-template <int EPI, int STP, bool OVL, int ABL = 0>
+// VB (round 6, verdict r5 item 4, A/B): the B operand staged through VGPRs instead of LDS-DMA -- phase 2 of
+// iteration i issues the 8 B pieces of tile i + 2 as plain buffer_load_dwordx4 into 32 VGPRs (same source
+// offsets, same slots), phase 1 of iteration i + 1 writes them lane-linear into the B half of buffer
+// (i + 2) & 1 with ds_write_b128 at slots 8-22, before that phase's A pieces (so the compiler's own wait for
+// the loads counts no asm piece younger than them); the end-of-phase lgkmcnt(0) and the phase-2 barrier make
+// them visible exactly as the DMA pieces were.  Only the A operand stays DMA-fed.
+template <int EPI, int STP, bool OVL, int ABL = 0, bool VB = false>
 __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                            bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
                                                            int64_t ldb, int64_t ldc, int GM) {
@@ -215,6 +221,8 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
   f32x4 acc[8][8];
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
   int pm0 = 0, pn0 = 0;  // tile of the accumulators (for its epilogue)
+  u32x4 sb[8];           // VB: the B pieces of tile i + 2 between their load (phase 2) and ds_write (phase 1)
+  bool have_sb = false;
 
   // ---- epilogue of the 16-row block a of the tile (m0, n0): lane row r16, columns 8 q + 0..7 of each
   // 32-column block pair -> one 16-B store per pair; rows past M drop through the descriptor, columns
@@ -249,11 +257,17 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
   auto phase1 = [&](auto FIRST, uint32_t cur, __amdgpu_buffer_rsrc_t dra, uint32_t dlds, auto&& hook)
       __attribute__((always_inline)) {
     constexpr bool F = decltype(FIRST)::value;
+    const uint32_t nxt = BUFB - cur;  // VB: the buffer of tile i + 2 (= i & 1 = the other one)
 #pragma unroll
     for (int s = 0; s < 64; ++s) {
       const int a = s >> 3, b = s & 7;
       if constexpr (F) mma0(fb0[b], fa0[a], acc[a][b]);
       else mma(fb0[b], fa0[a], acc[a][b]);
+      if constexpr (VB) {
+        if (s >= 8 && s <= 22 && (s & 1) == 0 && have_sb)
+          *reinterpret_cast<u32x4*>(smem + nxt + (uint32_t)w * 1024u + OPB + (uint32_t)((s - 8) / 2) * PS +
+                                    (uint32_t)lane * 16u) = sb[(s - 8) / 2];
+      }
       if (!(ABL & 2)) {
         if (a_rd1_slot(s)) rd_a(cur, 1, (s - 1) / 2, fa1);
         if (b_rd1_slot(s)) rd_b(cur, 1, (s - 26) / 3, fb1);
@@ -289,10 +303,11 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
         else rd_b(nxt, 0, r - 8, fb0);
       }
       if (b_dma_slot(s) && !(ABL & 1)) {
-        if constexpr ((ABL & 4096) != 0) gdma_go(gpb, vob[(s - 3) / 4]);
+        if constexpr (VB) sb[(s - 3) / 4] = __builtin_amdgcn_raw_buffer_load_b128(drb, vob[(s - 3) / 4], 0, 0);
+        else if constexpr ((ABL & 4096) != 0) gdma_go(gpb, vob[(s - 3) / 4]);
         else dma_go(drb, vob[(s - 3) / 4]);
       }
-      if (b_dma_slot(s + 1) && !(ABL & 1)) set_m0(dlds + OPB + (uint32_t)((s + 1 - 3) / 4) * PS);
+      if (!VB && b_dma_slot(s + 1) && !(ABL & 1)) set_m0(dlds + OPB + (uint32_t)((s + 1 - 3) / 4) * PS);
       if (s == 30) hook();
       if constexpr (L) {
         if (b == 4 && a > 0) epi(a - 1, pm0, pn0);
@@ -303,6 +318,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w128_kernel(const bf16_t* __restr
       drain();
       epi(7, pm0, pn0);
     }
+    if constexpr (VB) have_sb = true;
   };
 
   // ---- prologue: tiles 0 and 1 staged, tile 0 landed, its k-step 0 in F0
@@ -396,18 +412,22 @@ int num_cus_w128() {
 int g_w128_nt = 1;   // non-temporal C stores
 int g_w128_ovl = 1;  // epilogue woven into each tile's last phase (0: between the tiles)
 int g_w128_abl = 0;  // ablation variants (profiling only; -DND_ABLATION builds): nd_gemm_w128_set_ablation
+int g_w128_vb = [] {  // B operand staged through VGPRs (A/B; nd_gemm_w128_set_vb / ND_GEMM_W128_VB)
+  const char* e = getenv("ND_GEMM_W128_VB");
+  return e ? atoi(e) : 0;
+}();
 
-template <int EPI, int STP, bool OVL, int ABL = 0>
+template <int EPI, int STP, bool OVL, int ABL = 0, bool VB = false>
 int launch_w128_v(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
                   hipStream_t s) {
   const size_t lds = 2 * (size_t)BUFB0;  // 128 KiB
   static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&gemm_w128_kernel<EPI, STP, OVL, ABL>), hipFuncAttributeMaxDynamicSharedMemorySize,
+      reinterpret_cast<const void*>(&gemm_w128_kernel<EPI, STP, OVL, ABL, VB>), hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)lds);
   if (attr != hipSuccess) return (int)attr;
   const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   const int grid = tiles < num_cus_w128() ? tiles : num_cus_w128();
-  hipLaunchKernelGGL((gemm_w128_kernel<EPI, STP, OVL, ABL>), dim3(grid), dim3(256), lds, s, (const bf16_t*)A,
+  hipLaunchKernelGGL((gemm_w128_kernel<EPI, STP, OVL, ABL, VB>), dim3(grid), dim3(256), lds, s, (const bf16_t*)A,
                      (const bf16_t*)B, (bf16_t*)C, M, N, K, lda, ldb, ldc, g_w128_group_m);
   ND_LAUNCH_CHECK();
 }
@@ -430,6 +450,8 @@ int launch_w128(const void* A, const void* B, void* C, int M, int N, int K, int6
     }
   }
 #endif
+  if (g_w128_vb && g_w128_ovl && g_w128_nt && K >= 2 * TK)
+    return launch_w128_v<EPI, 2, true, 0, true>(A, B, C, M, N, K, lda, ldb, ldc, s);
   if (g_w128_ovl && K >= 2 * TK)
     return g_w128_nt ? launch_w128_v<EPI, 2, true>(A, B, C, M, N, K, lda, ldb, ldc, s)
                      : launch_w128_v<EPI, 0, true>(A, B, C, M, N, K, lda, ldb, ldc, s);
@@ -459,6 +481,14 @@ ND_API int nd_gemm_w128_set_ablation(int v) {
 #endif
   const int old = g_w128_abl;
   g_w128_abl = v;
+  return old;
+}
+
+// 1: the B operand staged through VGPRs (VB above; the epilogue-in-last-phase, non-temporal form only); returns
+// the previous setting
+ND_API int nd_gemm_w128_set_vb(int v) {
+  const int old = g_w128_vb;
+  if (v >= 0) g_w128_vb = v;
   return old;
 }
 

@@ -188,6 +188,7 @@ def _declare(L: ctypes.CDLL):
         "nd_gemm_w128": [P, P, P, I, I, I, L64, L64, L64, P],
         "nd_gemm_w128_set": [I, I, I],
         "nd_gemm_w128_set_ablation": [I],
+        "nd_gemm_w128_set_vb": [I],
         # weight-gradient GEMM
         "nd_wgrad_splits": [I, I, I],
         "nd_wgrad_f8_splits": [I, I, I],

@@ -295,6 +295,12 @@ def wgrad_f8(gw: torch.Tensor, dy8: torch.Tensor, x8: torch.Tensor, s_dy: torch.
                              _ext.stream_ptr(gw.device)), "nd_wgrad_f8")
 
 
+def set_w128_vb(v: int) -> int:
+    """1: the w128 kernel stages its B operand through VGPRs (buffer_load + ds_write) instead of LDS-DMA, the
+    A operand stays DMA-fed (A/B, round 6); 0: both DMA-fed (default).  Returns the previous setting."""
+    return int(_ext.lib().nd_gemm_w128_set_vb(int(v)))
+
+
 def set_w128_ablation(v: int) -> int:
     """Ablation builds of the w128 kernel (profiling only -- WRONG results): 1 no LDS-DMA, 2 no fragment
     reads, 4 no barriers, 8 no epilogue stores, 16 no vmcnt waits in the loop, 31 all; 0 = the kernel."""

@@ -125,8 +125,9 @@ def workloads(what):
         OUTPUTS["cast_e5m2"] = (q8,)
     elif what == "wgrad":
         from nanodiloco_amd.ops.gemm import wgrad
+        # lm: 500 output tiles -> one split (C += acc in place, the S == 1 epilogue)
         for name, (M, N) in {"qkv": (3072, 1024), "o": (1024, 1024), "gate_up": (5376, 1024),
-                             "down": (1024, 2688)}.items():
+                             "down": (1024, 2688), "lm": (32000, 1024)}.items():
             dy = torch.randn(32768, M, device="cuda").bfloat16()
             xx = torch.randn(32768, N, device="cuda").bfloat16()
             gw = torch.zeros(M, N, device="cuda")

@@ -55,6 +55,17 @@ def w128o(x, w, out):
         G.set_w128(ovl=0)
 
 
+def w128vb(x, w, out):
+    """the w128 kernel (epilogue in the last phase) with its B operand staged through VGPRs"""
+    G.set_w128(ovl=1)
+    old = G.set_w128_vb(1)
+    try:
+        return G.gemm_w128(x, w, out)
+    finally:
+        G.set_w128_vb(old)
+        G.set_w128(ovl=0)
+
+
 def check():
     torch.manual_seed(0)
     bad = 0
@@ -64,7 +75,8 @@ def check():
         a, b = r(m, k), r(n, k) * 0.05
         ref = a.float() @ b.float().t()
         for nm, fn in (("gemm_pp", G.gemm_pp), ("gemm_w128", G.gemm_w128),
-                       ("gemm_w128o", lambda a_, b_: w128o(a_, b_, None))):
+                       ("gemm_w128o", lambda a_, b_: w128o(a_, b_, None)),
+                       ("gemm_w128vb", lambda a_, b_: w128vb(a_, b_, None))):
             y = fn(a, b)
             e = rel(y, ref, f"{nm} {m}x{n}x{k}")
             ok = e < 1e-2
@@ -178,7 +190,8 @@ def main():
         x, w = r(m, k), r(n, k) * 0.05
         out = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
         arms = {"blas": lambda: torch.mm(x, w.t(), out=out), "pp": lambda: G.gemm_pp(x, w, out),
-                "w128": lambda: G.gemm_w128(x, w, out), "w128o": lambda: w128o(x, w, out)}
+                "w128": lambda: G.gemm_w128(x, w, out), "w128o": lambda: w128o(x, w, out),
+                "w128vb": lambda: w128vb(x, w, out)}
         cases.append((name, 2.0 * m * n * k, arms))
 
     plain("qkv fwd", M, qkv_n, d)

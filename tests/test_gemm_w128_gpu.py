@@ -83,3 +83,20 @@ def test_gemm_w128_identity_asymmetric():
     b = torch.randn(n, n, device=DEV).bfloat16()
     c = G.gemm_w128(a, b)
     assert torch.equal(c, b.t().contiguous())
+
+
+@pytest.mark.parametrize("M,N,K", [s for s in SHAPES if s[2] >= 128])
+def test_gemm_w128_vgpr_staged_b_bitwise(M, N, K):
+    """The B operand staged through VGPRs (buffer_load + ds_write, round 6 A/B) writes the same LDS image as the
+    LDS-DMA pieces: bitwise the same output (the variant runs with the epilogue inside the last phase; with the
+    between-tiles placement of the fixture both calls take the DMA path)."""
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    c0 = G.gemm_w128(a, b)
+    old = G.set_w128_vb(1)
+    try:
+        c1 = G.gemm_w128(a, b)
+    finally:
+        G.set_w128_vb(old)
+    assert torch.equal(c0, c1)
+    assert rel(c1, a.float() @ b.float().t()) < 5e-3
