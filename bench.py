@@ -254,7 +254,7 @@ def main():
             "outer_step_wall_ms": round(1000.0 * dl.avg_sync_time, 3),
             "allreduce_calls_per_outer_step": dl.buckets_per_outer_step,
             "comm_backend": env.backend,
-            "comm_impl": env.comm_impl,
+            "comm_impl": dl.outer_comm.impl if dl.outer_comm.enabled else env.comm_impl,  # after any agreed fallback
             "rccl_calls": (dl.outer_comm.rccl.stats()["calls"] if dl.outer_comm.rccl is not None else None),
             "comm_dtype": a.comm_dtype,
             "model_tflops_per_gpu": round(mfu_flops / 1e12, 2),

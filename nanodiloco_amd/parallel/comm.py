@@ -103,8 +103,10 @@ class FlatCommunicator:
         self.impl = impl if self.enabled else "none"
         self.rccl = None
         if self.enabled and impl == "rccl":
-            from .rccl import communicator_for
-            self.rccl = communicator_for(group, device, timeout_s)
+            from .rccl import communicator_or_fallback
+            self.rccl = communicator_or_fallback(group, device, timeout_s)
+            if self.rccl is None:  # every member agreed to carry the bulk traffic on c10d instead
+                self.impl = "c10d"
 
     def check(self, what: str = "step boundary"):
         """Raise if the own RCCL communicator failed (see :meth:`parallel.rccl.RcclCommunicator.check`).

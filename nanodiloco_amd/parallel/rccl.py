@@ -234,6 +234,48 @@ def communicator_for(group, device: torch.device, timeout_s: float = 1800.0,
     return c
 
 
+def init_timeout_s(default: float = 300.0) -> float:
+    """How long a communicator's bootstrap may wait for its peers (``ND_COMM_INIT_TIMEOUT``, seconds).
+    RCCL's init takes seconds on one node; a bounded wait turns a peer that never joins into an error the
+    group can agree on (:func:`communicator_or_fallback`) instead of a job that hangs until its own limit."""
+    return float(os.environ.get("ND_COMM_INIT_TIMEOUT", default))
+
+
+def communicator_or_fallback(group, device: torch.device, timeout_s: float = 1800.0,
+                             high_priority: bool = True) -> Optional[RcclCommunicator]:
+    """The group's own communicator, or None when ANY member failed to create it -- decided together.
+
+    Every member tries ``communicator_for`` (bounded by :func:`init_timeout_s`), then the members take the
+    MIN of their success flags over the torch process group of ``group`` (the control plane, which already
+    works: it carried the unique id).  If one member failed, all of them drop the own communicator and the
+    caller moves its bulk traffic to c10d, so no member is left issuing RCCL calls its peers never join.
+    ``ND_COMM_FALLBACK=0`` makes a failure fatal instead (strict A/B runs)."""
+    err: Optional[BaseException] = None
+    c: Optional[RcclCommunicator] = None
+    key = tuple(_group_ranks(group))
+    try:
+        c = _COMMS.get(key)
+        if c is None:
+            c = RcclCommunicator(group, device, timeout_s, high_priority, init_timeout_s=init_timeout_s())
+            _COMMS[key] = c
+    except (RcclError, OSError) as e:
+        err, c = e, None
+    if os.environ.get("ND_COMM_FALLBACK", "1") == "0" and err is not None:
+        raise err
+    flag_dev = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    ok = torch.tensor([0 if c is None else 1], dtype=torch.int32, device=flag_dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if int(ok.item()) == 1:
+        return c
+    if c is not None:  # a peer failed: this member's communicator has no partner to talk to
+        c.destroy(abort=True)
+        _COMMS.pop(key, None)
+    import warnings
+    warnings.warn(f"own RCCL communicator for ranks {list(key)} unavailable "
+                  f"({'here: ' + str(err) if err is not None else 'on a peer'}); bulk traffic falls back to c10d")
+    return None
+
+
 def destroy_communicators(abort: bool = False):
     for c in list(_COMMS.values()):
         c.destroy(abort)

@@ -76,3 +76,47 @@ def test_unique_id_exchange_through_store_4_ranks():
     # every member of a group got the same id
     assert res[0]["inits"][1][2] == res[1]["inits"][1][2] and res[2]["inits"][1][2] == res[3]["inits"][1][2]
     assert res[0]["inits"][2][2] == res[2]["inits"][2][2] and res[1]["inits"][2][2] == res[3]["inits"][2][2]
+
+
+def _fallback(rank, world, fail_rank):
+    import torch
+    import torch.distributed as dist
+
+    from nanodiloco_amd.parallel import rccl
+    from nanodiloco_amd.parallel.comm import FlatCommunicator
+
+    dist.init_process_group("gloo")
+    fake = _FakeLib(rank)
+    destroyed = []
+    fake.nd_comm_destroy2 = _FakeFn(lambda h, abort: destroyed.append(int(abort)) or 0)
+    if rank == fail_rank:  # this member's bootstrap fails (e.g. its peers never joined in time)
+        fake.nd_comm_init2 = _FakeFn(lambda *a: 7)
+        fake.nd_comm_error_string = _FakeFn(lambda rc: b"fake init failure")
+    rccl._lib = fake
+    try:
+        fc = FlatCommunicator(None, world, bucket_mb=1.0, impl="rccl", device=torch.device("cpu"))
+        x = torch.full((1000,), float(rank + 1))
+        if fc.rccl is None:  # agreed fallback: the bulk traffic really runs on c10d (gloo here)
+            fc.all_reduce(x)
+        out = {"impl": fc.impl, "has_rccl": fc.rccl is not None, "sum": float(x[0]), "destroyed": destroyed,
+               "cached": len(rccl._COMMS)}
+        if fc.rccl is not None:
+            fc.rccl._h = None
+        rccl._COMMS.clear()
+        return out
+    finally:
+        rccl._lib = None
+
+
+def test_failed_bootstrap_on_one_member_moves_every_member_to_c10d():
+    res = run_ranks(_fallback, 3, 1)
+    for o in res:
+        assert o["impl"] == "c10d" and not o["has_rccl"] and o["cached"] == 0, o
+        assert o["sum"] == 6.0, o  # 1 + 2 + 3 through gloo
+    assert res[0]["destroyed"] == [1] and res[2]["destroyed"] == [1]  # survivors aborted their communicator
+    assert res[1]["destroyed"] == []
+
+
+def test_successful_bootstrap_keeps_own_communicator():
+    res = run_ranks(_fallback, 2, -1)
+    assert all(o["impl"] == "rccl" and o["has_rccl"] for o in res), res
