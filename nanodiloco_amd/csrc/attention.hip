@@ -972,7 +972,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
 
   const int nkb = (T + 127) / 128, bk_count = B * nkv, rep = nh / nkv;
   int kb, bk;  // order 1: the key blocks of one (batch, kv head) together on one XCD (Q / dO from L2)
-  if (order) {
+  if (order & 1) {
     const int id = xcd_remap(blockIdx.x, nkb * bk_count);
     bk = id / nkb;
     kb = id % nkb;
@@ -1124,7 +1124,7 @@ __global__ void __launch_bounds__(256, (HD >= 128 ? 1 : 2)) attn_bwd_dkdv_kernel
 #endif
 struct AttnEnv {
   int order = 1;        // ND_ATTN_ORDER: grid order (see attn_fwd_kernel)
-  int dkdv_order = ND_ATTN_DKDV_ORDER_DEFAULT;   // ND_ATTN_DKDV_ORDER: group the key blocks of one (batch, kv head)
+  int dkdv_order = ND_ATTN_DKDV_ORDER_DEFAULT;   // ND_ATTN_DKDV_ORDER: bit 0 group the key blocks of one (batch, kv head), bit 1 descending query walk
   float thr = 8.f;      // ND_ATTN_THR: deferred-max threshold (log2 units; 0 = move the max on every increase)
   bool fwd_reg = false; // ND_ATTN_FWD=r: register-staged forward
   int fwd_var = 32;     // ND_ATTN_ABL: 32 (cheaper mask / v_max3 tree, 1.007-1.024x) or 0 (plain)
@@ -1160,7 +1160,9 @@ static const AttnEnv g_attn = [] {
   return c;
 }();
 static int attn_order() { return g_attn.order; }
-static int dkdv_order(int nh, int nkv) { return g_attn.dkdv_order && nh == nkv; }
+// bit 0: a (batch, head)'s key blocks consecutive on one XCD (MHA only); bit 1: descending query walk
+// (LDS-DMA dK/dV kernel)
+static int dkdv_order(int nh, int nkv) { return ((g_attn.dkdv_order & 1) && nh == nkv ? 1 : 0) | (g_attn.dkdv_order & 2); }
 
 // wrong-result ablation builds only (timing): ABL bits of attn_fwd_kernel / attn_bwd_dkdv_dma_kernel
 #ifdef ND_ABLATION
@@ -1303,7 +1305,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && BQ == 6
 
   const int bk_count = B * nkv, rep = nh / nkv, nkb = (T + KB - 1) / KB;
   int kb, bk;  // see attn_bwd_dkdv_kernel
-  if (order) {
+  if (order & 1) {
     const int id = xcd_remap(blockIdx.x, nkb * bk_count);
     bk = id / nkb;
     kb = id % nkb;
@@ -1348,11 +1350,21 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && BQ == 6
   const int qstart = (kb * KB) / BQ * BQ;
   const int ntq = (T - qstart + BQ - 1) / BQ;
   const int nit = ntq * rep;
+  // order bit 1: walk the query tiles from the LAST one down to the diagonal.  Every key block of a head
+  // ends at query tile ntq - 1, so descending walks line the key blocks up on the SAME Q / dO tile at the
+  // same step (the ascending walk starts each on its own diagonal tile: key block kb reads tile q at step
+  // q - kb); with bit 0 (a head's key blocks consecutive on one XCD) the tile is then fetched once into
+  // that XCD's L2 and re-read there.  Only the fp32 accumulation order of dK / dV changes.
+  const bool desc = (order & 2) != 0;
+  auto qtile = [&](int it) __attribute__((always_inline)) {
+    const int r = it % ntq;
+    return desc ? ntq - 1 - r : r;
+  };
   ND_STAMP(Stamps stp; stp.start();)
   // part: 7 = everything; 1 = Q pieces, 2 = dO pieces, 4 = row statistics (ND_ATTN_X & 128 spreads them)
   auto issue = [&](int it, int part = 7) {
     const int head = kvh * rep + it / ntq;
-    const int q0 = qstart + (it % ntq) * BQ;
+    const int q0 = qstart + qtile(it) * BQ;
     const int buf = it % NB;
     const bf16_t* sq = Q + ((int64_t)b * T + q0) * ld + (int64_t)head * HD;
     const bf16_t* sd = dO + ((int64_t)b * T + q0) * ldo + (int64_t)head * HD;
@@ -1395,7 +1407,7 @@ __global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : (HD == 64 && BQ == 6
     if constexpr (!(ABL & 2)) __syncthreads();        // everyone's; and tile it-1's buffer is free
     ND_STAMP(stp.mark(1);)
     if constexpr (!(ABL & 1) && !SPREAD) if (it + NB - 1 < nit) issue(it + NB - 1);
-    const int q0 = qstart + (it % ntq) * BQ;
+    const int q0 = qstart + qtile(it) * BQ;
     const int buf = it % NB;
     const bf16_t* Qt = Qs + buf * (BQ * HD);
     const bf16_t* dOt = dOs + buf * (BQ * HD);
