@@ -224,6 +224,11 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
               const int t = (m0 + mr + aa * 16) % ep.T;
 #pragma unroll
               for (int j = 0; j < NJ; ++j) {
+                if constexpr ((ABL & 16384) != 0) {  // ablation: no table loads (wrong result, timing only)
+                  ctab[aa][j] = float4{0.5f, 0.25f, (float)t, (float)j};
+                  stab[aa][j] = float4{(float)q, 0.125f, 0.75f, (float)aa};
+                  continue;
+                }
                 ctab[aa][j] = *reinterpret_cast<const float4*>(ep.cosT + (int64_t)t * HD + j * 16 + 4 * q);
                 stab[aa][j] = *reinterpret_cast<const float4*>(ep.sinT + (int64_t)t * HD + j * 16 + 4 * q);
               }
@@ -824,6 +829,10 @@ int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_
               const PPEpi& ep, hipStream_t s) {
   if (g_pp_variant == 1024) return launch_pp_v<EPI, HD, 1024>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
 #ifdef ND_ABLATION
+  if constexpr (EPI == PP_ROPE) {  // epilogue ablations of the q|k|v + RoPE product: 8 none, 16384 no table loads
+    if (g_pp_variant == 8) return launch_pp_v<EPI, HD, 8>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    if (g_pp_variant == 16384) return launch_pp_v<EPI, HD, 16384>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+  }
   if constexpr (EPI == PP_DSWIGLU || EPI == PP_SWIGLU) {  // epilogue ablations of the fused MLP products
     if (g_pp_variant == 8) return launch_pp_v<EPI, HD, 8>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
     if (g_pp_variant == 4096) return launch_pp_v<EPI, HD, 4096>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
