@@ -278,7 +278,8 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
               const int rr = i * 8 + ((lane + z) >> 3);
               const u32x4 d = *reinterpret_cast<const u32x4*>(st + rr * 128 + ((lc ^ (rr & 7)) << 4));
               const int gr = g * 128 + (a - 1) * 16 + rr;
-              const uint32_t off = col < N ? (uint32_t)(((int64_t)gr * ldc + col) * 2) : 0x80000000u;
+              // ABL 8192 (ablation builds): every store out of range -- the epilogue's instructions without its HBM writes
+              const uint32_t off = col < N && (ABL & 8192) == 0 ? (uint32_t)(((int64_t)gr * ldc + col) * 2) : 0x80000000u;
               __builtin_amdgcn_raw_buffer_store_b128(d, cr, off, 0, STP);
             }
             asm volatile("" ::: "memory");
@@ -832,6 +833,7 @@ int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_
   if constexpr (EPI == PP_ROPE) {  // epilogue ablations of the q|k|v + RoPE product: 8 none, 16384 no table loads
     if (g_pp_variant == 8) return launch_pp_v<EPI, HD, 8>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
     if (g_pp_variant == 16384) return launch_pp_v<EPI, HD, 16384>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    if (g_pp_variant == 8192) return launch_pp_v<EPI, HD, 8192>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
   }
   if constexpr (EPI == PP_DSWIGLU || EPI == PP_SWIGLU) {  // epilogue ablations of the fused MLP products
     if (g_pp_variant == 8) return launch_pp_v<EPI, HD, 8>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
@@ -851,6 +853,7 @@ int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_
       case 16: return launch_pp_v<EPI, HD, 16>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       case 64: return launch_pp_v<EPI, HD, 64>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       case 128: return launch_pp_v<EPI, HD, 128>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+      case 8192: return launch_pp_v<EPI, HD, 8192>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
 #endif
       case 32: return launch_pp_v<EPI, HD, 32>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);    // plain-policy stores
       case 256: return launch_pp_v<EPI, HD, 256>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);  // direct stores
