@@ -76,6 +76,9 @@ constexpr uint32_t BUF_B = 4 * HALF_B;     // bytes of one K-tile buffer (64 KiB
 constexpr int LGKM0 = 0xC07F;              // s_waitcnt lgkmcnt(0), vmcnt / expcnt at their maxima
 
 enum : int { PP_STORE = 0, PP_ROPE = 1, PP_SWIGLU = 2, PP_DSWIGLU = 3 };
+#ifndef ND_MLP_COEF_DEFAULT
+#define ND_MLP_COEF_DEFAULT 0  // saved-tensor form of the fused SwiGLU pair (g_mlp_coef below)
+#endif
 
 struct PPEpi {
   const float* cosT;  // PP_ROPE: fp32 [T, hd] tables (HF cat(freqs, freqs) layout)
@@ -193,7 +196,13 @@ __device__ __forceinline__ float silu(float g) { return g * fast_sigmoid(g); }
 // of the tile at (m0, n0) -> the fused output(s).  Exactly NStores<EPI> 16-B buffer stores per wave
 // (the callers' counted waits rely on it); out-of-range lanes drop through the descriptor's record
 // count or an offset sentinel.  `smem` + 2 BUF_B + 4 KiB w: the wave's private C staging region.
-template <int EPI, int HD, int ABL, int F8 = 0, int Q = 0>
+// FORM (PP_SWIGLU / PP_DSWIGLU only, round 6): 0 -- the forward keeps gu = [gate | up] for the backward, which
+// recomputes sigmoid(gate) and the SwiGLU derivative per element; 1 (coefficient form) -- the forward, which has
+// sigmoid(gate) in hand for act, keeps [A | B] instead, A = up s (1 + gate (1 - s)) = d act / d gate and
+// B = gate s = d act / d up (s = sigmoid(gate), all from the bf16-rounded gate / up act is computed from), so the
+// backward epilogue is d(gate) = d(act) A, d(up) = d(act) B: two multiplies per unit instead of a sigmoid and ten
+// more VALU.  Same buffer, same traffic; the two launchers read one switch (g_mlp_coef) so they always agree.
+template <int EPI, int HD, int ABL, int F8 = 0, int Q = 0, int FORM = 0>
 __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __restrict__ C, int M, int N,
                                             int64_t ldc, const PPEpi& ep, int m0, int n0, int g, int wn, int w,
                                             int lane, char* smem, float sc, float qs, float& qmax) {
@@ -310,7 +319,15 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
           for (int r = 0; r < 4; ++r) {
             g2[j][r] = rbf(F8 != 0 ? acc[a][j][r] * sc : acc[a][j][r]);  // act from the rounded gate / up: what the backward reads
             u2[j][r] = rbf(F8 != 0 ? acc[a][j + 2][r] * sc : acc[a][j + 2][r]);
-            y2[j][r] = silu(g2[j][r]) * u2[j][r];
+            if constexpr (FORM == 1) {
+              const float sg = fast_sigmoid(g2[j][r]), sl = g2[j][r] * sg;  // sl = silu(gate), bitwise silu()
+              y2[j][r] = sl * u2[j][r];
+              const float cg = (u2[j][r] * sg) * (1.f + g2[j][r] * (1.f - sg));  // A (stored where gate was)
+              g2[j][r] = cg;
+              u2[j][r] = sl;                                                   // B (stored where up was)
+            } else {
+              y2[j][r] = silu(g2[j][r]) * u2[j][r];
+            }
           }
         const bool okst = ok && (ABL & 8192) == 0;  // ABL 8192: stores out of range (no HBM writes; timing only)
         const uint32_t og = okst ? (uint32_t)(((int64_t)mr * ldc + f) * 2) : 0x80000000u;
@@ -404,9 +421,14 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
             const float d = e < 4 ? d0[e] : d1[e - 4];
             const float gg = (e & 1) ? hi_bf(gw[e >> 1]) : lo_bf(gw[e >> 1]);
             const float uu = (e & 1) ? hi_bf(uw[e >> 1]) : lo_bf(uw[e >> 1]);
-            const float sg = fast_sigmoid(gg);
-            du[e] = d * gg * sg;
-            dg[e] = d * uu * sg * (1.f + gg * (1.f - sg));
+            if constexpr (FORM == 1) {  // gg = A, uu = B (coefficient form, see pp_epilogue)
+              dg[e] = d * gg;
+              du[e] = d * uu;
+            } else {
+              const float sg = fast_sigmoid(gg);
+              du[e] = d * gg * sg;
+              dg[e] = d * uu * sg * (1.f + gg * (1.f - sg));
+            }
           }
           if constexpr (Q != 0) {
             // e5m2 d(gate | up) instead of the bf16 one: bf16-rounded, scaled, two 8-B stores
@@ -467,7 +489,7 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
 // the q|k|v epilogue per wave: its 64 columns are all q / k (RoPE) or all v (rope_cols % 64 == 0), so a
 // wave-uniform branch picks the RoPE body or the plain store body -- the v waves load no tables, whose
 // vmcnt waits would also drain the LDS-DMA pieces issued just before them (both bodies store NStores = 16)
-template <int EPI, int HD, int ABL, int F8 = 0, int Q = 0>
+template <int EPI, int HD, int ABL, int F8 = 0, int Q = 0, int FORM = 0>
 __device__ __forceinline__ void pp_epilogue_any(const f32x4 (&acc)[8][4], bf16_t* __restrict__ C, int M, int N,
                                                 int64_t ldc, const PPEpi& ep, int m0, int n0, int g, int wn, int w,
                                                 int lane, char* smem, float sc, float qs, float& qmax) {
@@ -478,7 +500,7 @@ __device__ __forceinline__ void pp_epilogue_any(const f32x4 (&acc)[8][4], bf16_t
     else
       pp_epilogue<PP_STORE, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
   } else {
-    pp_epilogue<EPI, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
+    pp_epilogue<EPI, HD, ABL, F8, Q, FORM>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
   }
 }
 
@@ -488,7 +510,7 @@ __device__ __forceinline__ void pp_epilogue_any(const f32x4 (&acc)[8][4], bf16_t
 // LDS loads: bitwise the same, 1.004-1.011x on the fused kernels, profiles/r4_gdma_ab.md)
 // F8 (fp8 operands, one 16x16x128 MFMA per 128-deep K-tile of the same 128-B LDS rows): 0 bf16; 1 A e4m3,
 // B e4m3 (forward); 2 A e5m2, B e4m3 (input gradient).  A / B are then byte arrays, lda / ldb in bytes.
-template <int EPI, int HD, int ABL = 0, int F8 = 0, int Q = 0>
+template <int EPI, int HD, int ABL = 0, int F8 = 0, int Q = 0, int FORM = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restrict__ A_, const bf16_t* __restrict__ B_,
                                                          bf16_t* __restrict__ C, int M, int N, int K, int64_t lda,
                                                          int64_t ldb, int64_t ldc, PPEpi ep, int GM) {
@@ -716,7 +738,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
       } else {
         int m0, n0;
         coords(first + (lt - 1) * G, m0, n0);
-        pp_epilogue_any<EPI, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
+        pp_epilogue_any<EPI, HD, ABL, F8, Q, FORM>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
       }
       // the accumulators are free only after the epilogue has read them: keep the fragment reads
       // (96 VGPRs) from being hoisted into it
@@ -768,7 +790,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(const bf16_t* __restric
   if constexpr ((ABL & 8) == 0) {
     int m0, n0;
     coords(first + (my_tiles - 1) * G, m0, n0);
-    pp_epilogue_any<EPI, HD, ABL, F8, Q>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
+    pp_epilogue_any<EPI, HD, ABL, F8, Q, FORM>(acc, C, M, N, ldc, ep, m0, n0, g, wn, w, lane, smem, sc, qs, qmax);
   }
   if (g == 0 && !(ABL & 4)) bar();  // group 1 ran one barrier more
   if constexpr (Q != 0) {  // one amax partial per wave (vector atomic on an ordered-int view)
@@ -810,17 +832,17 @@ int g_pp_variant = [] {
 }();
 
 
-template <int EPI, int HD, int ABL, int F8 = 0, int Q = 0>
+template <int EPI, int HD, int ABL, int F8 = 0, int Q = 0, int FORM = 0>
 int launch_pp_v(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
                 const PPEpi& ep, hipStream_t s) {
   const size_t lds = 2 * (size_t)BUF_B + ((ABL & 256) ? 0 : 8 * 4096);  // 128 KiB + 32 KiB C staging
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<EPI, HD, ABL, F8, Q>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<EPI, HD, ABL, F8, Q, FORM>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return (int)attr;
   const int tcols = EPI == PP_SWIGLU ? 128 : TN;
   const int tiles = ((M + TM - 1) / TM) * ((N + tcols - 1) / tcols);
   const int grid = tiles < num_cus_pp() ? tiles : num_cus_pp();
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, HD, ABL, F8, Q>), dim3(grid), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, HD, ABL, F8, Q, FORM>), dim3(grid), dim3(512), lds, s, (const bf16_t*)A, (const bf16_t*)B,
                      (bf16_t*)C, M, N, K, lda, ldb, ldc, ep, g_pp_group_m);
   ND_LAUNCH_CHECK();
 }
@@ -894,6 +916,21 @@ ND_API int nd_gemm_pp_rope(const void* A, const void* B, void* C, int M, int N, 
                   : launch_pp<PP_ROPE, 32>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
 }
 
+// The SwiGLU pair's saved-tensor form (FORM of pp_epilogue): 0 gate / up, 1 the coefficient form.  ONE switch for
+// the forward and backward launchers of every dtype, so the two sides of a step always agree; ND_MLP_COEF at load,
+// nd_mlp_coef_set for A/B (set it only between steps: a forward saved in one form must be read back in it).
+int g_mlp_coef = [] {
+  const char* e = getenv("ND_MLP_COEF");
+  return e ? (atoi(e) != 0) : ND_MLP_COEF_DEFAULT;
+}();
+template <int EPI, int F8 = 0, int Q = 0>
+int launch_mlp(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
+               const PPEpi& ep, hipStream_t s) {
+  if (g_mlp_coef) return launch_pp_v<EPI, 64, 0, F8, Q, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+  if constexpr (F8 == 0) return launch_pp<EPI>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);  // incl. the A/B variants
+  else return launch_pp_v<EPI, 64, 0, F8, Q>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+}
+
 // gate|up projection + SwiGLU: B = fused weight [2F, K] (gate rows then up rows), gu = C [M, 2F]
 // (ldc), act [M, F] (ld_act).  F % 8 == 0.
 ND_API int nd_gemm_pp_swiglu(const void* A, const void* B, void* gu, void* act, int M, int F, int K, int64_t lda,
@@ -903,7 +940,7 @@ ND_API int nd_gemm_pp_swiglu(const void* A, const void* B, void* gu, void* act, 
     return (int)hipErrorInvalidValue;
   PPEpi ep{};
   ep.act = (bf16_t*)act; ep.ld_act = ld_act;
-  return launch_pp<PP_SWIGLU>(A, B, gu, M, F, K, lda, ldb, ldc, ep, s);
+  return launch_mlp<PP_SWIGLU>(A, B, gu, M, F, K, lda, ldb, ldc, ep, s);
 }
 
 // down-projection input gradient fused with the SwiGLU backward: d(act) = A . B^T (A = dY [M, K],
@@ -915,7 +952,7 @@ ND_API int nd_gemm_pp_dswiglu(const void* A, const void* B, const void* gu, void
     return (int)hipErrorInvalidValue;
   PPEpi ep{};
   ep.gu = (const bf16_t*)gu; ep.ld_gu = ld_gu;
-  return launch_pp<PP_DSWIGLU>(A, B, dgu, M, F, K, lda, ldb, ld_dgu, ep, s);
+  return launch_mlp<PP_DSWIGLU>(A, B, dgu, M, F, K, lda, ldb, ld_dgu, ep, s);
 }
 
 // ---- fp8 operands (A, B byte arrays, lda / ldb in bytes = elements): C = bf16(sa sb A . B^T) and the same
@@ -961,7 +998,7 @@ ND_API int nd_gemm_pp_swiglu_f8(const void* A, const void* B, void* gu, void* ac
     return (int)hipErrorInvalidValue;
   PPEpi ep{};
   ep.act = (bf16_t*)act; ep.ld_act = ld_act; ep.sa = sa; ep.sb = sb;
-  return launch_pp_v<PP_SWIGLU, 64, 0, 1>(A, B, gu, M, F, K, lda, ldb, ldc, ep, s);
+  return launch_mlp<PP_SWIGLU, 1>(A, B, gu, M, F, K, lda, ldb, ldc, ep, s);
 }
 
 // A = dY in e5m2 (fa = 1) or e4m3 (fa = 0)
@@ -973,7 +1010,8 @@ ND_API int nd_gemm_pp_dswiglu_f8(const void* A, const void* B, const void* gu, v
     return (int)hipErrorInvalidValue;
   PPEpi ep{};
   ep.gu = (const bf16_t*)gu; ep.ld_gu = ld_gu; ep.sa = sa; ep.sb = sb;
-  return launch_pp8<PP_DSWIGLU>(fa, A, B, dgu, M, F, K, lda, ldb, ld_dgu, ep, s);
+  return fa == 0 ? launch_mlp<PP_DSWIGLU, 1>(A, B, dgu, M, F, K, lda, ldb, ld_dgu, ep, s)
+                 : launch_mlp<PP_DSWIGLU, 2>(A, B, dgu, M, F, K, lda, ldb, ld_dgu, ep, s);
 }
 
 // Q forms: the SwiGLU output as e4m3 act8 [M, F] (ld_q8) INSTEAD of the bf16 act / the d(gate|up) as e5m2
@@ -988,7 +1026,7 @@ ND_API int nd_gemm_pp_swiglu_f8q(const void* A, const void* B, void* gu, void* a
   PPEpi ep{};
   ep.sa = sa; ep.sb = sb; ep.q8 = (uint8_t*)act8; ep.ld_q8 = ld_q8; ep.qscale = qscale; ep.qamax = qamax;
   ep.qparts = qparts;
-  return launch_pp_v<PP_SWIGLU, 64, 0, 1, 1>(A, B, gu, M, F, K, lda, ldb, ldc, ep, s);
+  return launch_mlp<PP_SWIGLU, 1, 1>(A, B, gu, M, F, K, lda, ldb, ldc, ep, s);
 }
 
 ND_API int nd_gemm_pp_dswiglu_f8q(const void* A, const void* B, const void* gu, void* dgu8, int M, int F, int K,
@@ -1003,8 +1041,8 @@ ND_API int nd_gemm_pp_dswiglu_f8q(const void* A, const void* B, const void* gu, 
   ep.gu = (const bf16_t*)gu; ep.ld_gu = ld_gu; ep.sa = sa; ep.sb = sb; ep.q8 = (uint8_t*)dgu8; ep.ld_q8 = ld_q8;
   ep.qscale = qscale; ep.qamax = qamax; ep.qparts = qparts;
   // C (the bf16 dgu) is not written: the Q epilogue stores through ep.q8 only
-  return fa == 0 ? launch_pp_v<PP_DSWIGLU, 64, 0, 1, 1>(A, B, dgu8, M, F, K, lda, ldb, 2 * (int64_t)F, ep, s)
-                 : launch_pp_v<PP_DSWIGLU, 64, 0, 2, 1>(A, B, dgu8, M, F, K, lda, ldb, 2 * (int64_t)F, ep, s);
+  return fa == 0 ? launch_mlp<PP_DSWIGLU, 1, 1>(A, B, dgu8, M, F, K, lda, ldb, 2 * (int64_t)F, ep, s)
+                 : launch_mlp<PP_DSWIGLU, 2, 1>(A, B, dgu8, M, F, K, lda, ldb, 2 * (int64_t)F, ep, s);
 }
 
 // returns the previous variant, or -1 (nothing changed) for a variant this build does not contain
@@ -1012,6 +1050,13 @@ ND_API int nd_gemm_pp_set_variant(int v) {
   if (!pp_variant_ok(v)) return -1;
   const int old = g_pp_variant;
   g_pp_variant = v;
+  return old;
+}
+
+// the SwiGLU saved-tensor form (see g_mlp_coef); v < 0 only reads it.  Returns the previous setting.
+ND_API int nd_mlp_coef_set(int v) {
+  const int old = g_mlp_coef;
+  if (v >= 0) g_mlp_coef = v != 0;
   return old;
 }
 

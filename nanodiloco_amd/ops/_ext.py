@@ -179,6 +179,7 @@ def _declare(L: ctypes.CDLL):
         "nd_gemm_pp_swiglu_f8": [P, P, P, P, I, I, I, L64, L64, L64, L64, P, P, P],
         "nd_gemm_pp_dswiglu_f8": [P, P, P, P, I, I, I, L64, L64, L64, L64, P, P, I, P],
         "nd_gemm_pp_set_group_m": [I],
+        "nd_mlp_coef_set": [I],
         "nd_probe_tr8": [P, P, P, P],
         "nd_gemm_pp_swiglu_f8q": [P, P, P, P, I, I, I, L64, L64, L64, L64, P, P, P, P, I, P],
         "nd_gemm_pp_dswiglu_f8q": [P, P, P, P, I, I, I, L64, L64, L64, L64, P, P, I, P, P, I, P],

@@ -208,6 +208,19 @@ def set_pp_variant(v: int) -> int:
     return int(_ext.lib().nd_gemm_pp_set_variant(int(v)))
 
 
+def set_mlp_coef(v: int) -> int:
+    """Saved-tensor form of the fused SwiGLU pair (gemm_pp_swiglu* -> gemm_pp_dswiglu*, every dtype): 0 the
+    forward keeps gu = [gate | up] and the backward recomputes sigmoid(gate); 1 the forward keeps the SwiGLU
+    derivative coefficients [A | B] (A = d act / d gate, B = d act / d up) in the same buffer, so the backward is
+    two multiplies per unit.  Set it only between steps (a saved tensor must be read back in its own form);
+    v < 0 only reads it.  Returns the previous setting."""
+    return int(_ext.lib().nd_mlp_coef_set(int(v)))
+
+
+def mlp_coef() -> int:
+    return set_mlp_coef(-1)
+
+
 def set_pp_group_m(g: int) -> int:
     """m-panels per tile group of the ping-pong kernel (XCD L2 locality); returns the old value."""
     return int(_ext.lib().nd_gemm_pp_set_group_m(int(g)))
