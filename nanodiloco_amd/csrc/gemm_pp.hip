@@ -77,7 +77,8 @@ constexpr int LGKM0 = 0xC07F;              // s_waitcnt lgkmcnt(0), vmcnt / expc
 
 enum : int { PP_STORE = 0, PP_ROPE = 1, PP_SWIGLU = 2, PP_DSWIGLU = 3 };
 #ifndef ND_MLP_COEF_DEFAULT
-#define ND_MLP_COEF_DEFAULT 0  // saved-tensor form of the fused SwiGLU pair (g_mlp_coef below)
+#define ND_MLP_COEF_DEFAULT 1  // saved-tensor form of the fused SwiGLU pair (g_mlp_coef below): the coefficient form
+                               // (down dgrad + SwiGLU backward 1.046x, step +0.2 %: profiles/r6_mlp_coef_ab.md)
 #endif
 
 struct PPEpi {

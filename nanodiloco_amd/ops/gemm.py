@@ -212,8 +212,8 @@ def set_mlp_coef(v: int) -> int:
     """Saved-tensor form of the fused SwiGLU pair (gemm_pp_swiglu* -> gemm_pp_dswiglu*, every dtype): 0 the
     forward keeps gu = [gate | up] and the backward recomputes sigmoid(gate); 1 the forward keeps the SwiGLU
     derivative coefficients [A | B] (A = d act / d gate, B = d act / d up) in the same buffer, so the backward is
-    two multiplies per unit.  Set it only between steps (a saved tensor must be read back in its own form);
-    v < 0 only reads it.  Returns the previous setting."""
+    two multiplies per unit (the default since round 6: profiles/r6_mlp_coef_ab.md).  Set it only between steps (a
+    saved tensor must be read back in its own form); v < 0 only reads it.  Returns the previous setting."""
     return int(_ext.lib().nd_mlp_coef_set(int(v)))
 
 

@@ -311,7 +311,9 @@ def mlp_fused_supported(y: torch.Tensor, w_gu: torch.Tensor, wt_gu, w_down: torc
 class MLPFn(torch.autograd.Function):
     """The whole SwiGLU MLP on the own GEMM with both activation passes fused away:
 
-      forward   gu, act = [gate|up GEMM + SwiGLU epilogue](y)      (gu kept for the backward)
+      forward   gu, act = [gate|up GEMM + SwiGLU epilogue](y)      (gu kept for the backward; by default in the
+                                                                  coefficient form [d act/d gate | d act/d up],
+                                                                  ops.gemm.set_mlp_coef)
                 m       = act . W_down^T
       backward  dgu     = [down dgrad GEMM + SwiGLU-backward epilogue](dm, W_down^T copy, gu)
                           -- d(act) is never stored

@@ -18,8 +18,10 @@ def _hip(hip_lib):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ops.set_backend("hip")
+    form = G.set_mlp_coef(0)  # the gate / up saved form of the SwiGLU pair (the coefficient form: test_mlp_coef_gpu.py)
     torch.manual_seed(0)
     yield
+    G.set_mlp_coef(form)
     ops.set_backend("auto")
 
 
