@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""In-process A/B of the ping-pong GEMM's C-store cache policy (ND_GEMM_PP_VARIANT / ops.gemm.set_pp_variant:
+0 nt stores, 2048 sc1 + nt, 2080 sc1 -- sc1 stores do not keep the written lines in the XCD's L2): the plain
+Llama-150M products at 131,072 tokens on the own kernel and the three fused-epilogue products, interleaved,
+median of 5 rounds.
+
+    python scripts/store_policy_ab.py
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nanodiloco_amd import ops  # noqa: E402
+from nanodiloco_amd.ops import gemm as G  # noqa: E402
+from nanodiloco_amd.ops.attention import rope_cache  # noqa: E402
+
+
+def timed(fn, iters=8):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def main():
+    ops.set_backend("hip")
+    M, d, F, V = 131072, 1024, 2688, 32000
+    r = lambda *s: ((torch.rand(*s, device="cuda") * 2 - 1) * 0.05).bfloat16()  # noqa: E731
+    x, xf, xqkv, xgu = r(M, d), r(M, F), r(M, 3 * d), r(M, 2 * F)
+    wo, wdn, wqkvT, wguT, wqkv, wgu, wdT, wlm, wlmT = (r(d, d), r(d, F), r(d, 3 * d), r(d, 2 * F), r(3 * d, d),
+                                                       r(2 * F, d), r(F, d), r(V, d), r(d, V))
+    xl = r(M // 2, d)
+    dl = r(M // 2, V)
+    gu = r(M, 2 * F)
+    cos, sin = rope_cache(1024, 64, 10000.0, None, "cuda")
+    arms = {
+        "o fwd": lambda: G.gemm_pp(x, wo), "down fwd": lambda: G.gemm_pp(xf, wdn),
+        "qkv dgrad": lambda: G.gemm_pp(xqkv, wqkvT), "gu dgrad": lambda: G.gemm_pp(xgu, wguT),
+        "lm logits 64k": lambda: G.gemm_pp(xl, wlm), "lm dgrad 64k": lambda: G.gemm_pp(dl, wlmT),
+        "qkv+rope": lambda: G.gemm_pp_rope(x, wqkv, cos, sin, 1024, 64, 2 * d),
+        "gu+swiglu": lambda: G.gemm_pp_swiglu(x, wgu), "down dgrad+dswiglu": lambda: G.gemm_pp_dswiglu(x, wdT, gu),
+    }
+    variants = (0, 2048, 2080)
+    for k in ("o fwd", "qkv+rope", "gu+swiglu", "down dgrad+dswiglu"):  # the policy must not change a bit
+        outs = []
+        for v in variants:
+            G.set_pp_variant(v)
+            o = arms[k]()
+            outs.append([t.clone() for t in (o if isinstance(o, tuple) else (o,))])
+        assert all(torch.equal(a, b) for o in outs[1:] for a, b in zip(outs[0], o)), k
+    print("outputs bitwise equal across the store policies", flush=True)
+    res = {}
+    old = G.set_pp_variant(0)
+    for _ in range(5):
+        for v in variants:
+            assert G.set_pp_variant(v) >= 0, v
+            for k, fn in arms.items():
+                res.setdefault((k, v), []).append(timed(fn))
+    G.set_pp_variant(old)
+    tot = {v: 0.0 for v in variants}
+    for k in arms:
+        t = {v: sorted(res[(k, v)])[2] for v in variants}
+        for v in variants:
+            tot[v] += t[v]
+        print(f"{k:19s} " + " | ".join(f"v{v} {t[v]:8.1f} us ({t[0] / t[v]:.3f}x)" for v in variants), flush=True)
+    print("total " + " | ".join(f"v{v} {tot[v]:8.1f} us ({tot[0] / tot[v]:.3f}x)" for v in variants), flush=True)
+
+
+if __name__ == "__main__":
+    main()
