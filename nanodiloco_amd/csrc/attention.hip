@@ -755,8 +755,11 @@ __global__ void __launch_bounds__(256) attn_bwd_pre_kernel(const bf16_t* __restr
 // half of O, dots, and one lane^32 exchange gives delta = rowsum(dO * O); the kernel then writes
 // -delta and -LSE/c (the seeds of the dK/dV kernel, which therefore runs after this one).
 // NW: waves per workgroup (8 = 256-query blocks, LDS-DMA only; see attn_fwd_kernel)
+#ifndef ND_ATTN_DQ_OCC
+#define ND_ATTN_DQ_OCC 2  // waves / SIMD the head_dim-64 dQ kernel is compiled for (A/B)
+#endif
 template <int HD, bool ROPE, bool ROPE_OUT, bool DMA = false, bool PRE = false, bool PAD = false, int NW = 4>  // DMA: LDS-DMA K/V staging
-__global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : 2)) attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+__global__ void __launch_bounds__(64 * NW, (HD >= 128 ? 1 : HD == 64 ? ND_ATTN_DQ_OCC : 2)) attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                              const bf16_t* __restrict__ V, const bf16_t* __restrict__ dO,
                                                              const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                              bf16_t* __restrict__ dQ, int B, int nh, int nkv, int T,
