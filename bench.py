@@ -92,6 +92,9 @@ def parse():
                     help="RoPE in the q|k|v GEMM epilogue (own kernel) vs a separate rotation pass")
     ap.add_argument("--fused-mlp", type=int, default=1, choices=[0, 1],
                     help="SwiGLU in the gate|up GEMM epilogue and its backward in the down dgrad epilogue")
+    ap.add_argument("--mlp-coef", type=int, default=-1, choices=[-1, 0, 1],
+                    help="saved-tensor form of the fused SwiGLU pair: 1 derivative coefficients (the library default, "
+                         "profiles/r6_mlp_coef_ab.md), 0 gate / up; -1 keeps the library's setting (ND_MLP_COEF)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3/e5m2) decoder projections (BASELINE config 5)")
     ap.add_argument("--fp8-wgrad", type=int, default=1, choices=[0, 1],
                     help="with --fp8: weight-gradient GEMMs in fp8 too (own kernel on the token-major fp8 "
@@ -112,11 +115,25 @@ def parse():
     return ap.parse_args()
 
 
+def _mlp_form():
+    """'coef' / 'gate_up': the fused SwiGLU pair's saved-tensor form that ran (None without the HIP library)."""
+    if not torch.cuda.is_available():
+        return None
+    try:
+        from nanodiloco_amd.ops.gemm import mlp_coef
+        return "coef" if mlp_coef() else "gate_up"
+    except Exception:
+        return None
+
+
 def main():
     a = parse()
     # kernel-path switches the trainer does not own (A/B flags); set before the model is built
     ops.set_proj_gemm(a.proj_gemm)
     ops.set_fused_epilogues(rope=bool(a.fused_rope), mlp=bool(a.fused_mlp))
+    if a.mlp_coef >= 0 and torch.cuda.is_available():
+        from nanodiloco_amd.ops.gemm import set_mlp_coef
+        set_mlp_coef(a.mlp_coef)
     ops.set_dgrad_transposed(bool(a.dgrad_t))
     ops.set_attn_fused_stats(bool(a.attn_fused_stats))
     if a.fp8:
@@ -266,6 +283,7 @@ def main():
             "deterministic": bool(a.deterministic),
             "proj_gemm": ops.proj_gemm(),
             "fused_epilogues": ops.fused_epilogues(),
+            "mlp_saved_form": _mlp_form(),
             "fp8_gemm": a.fp8_gemm if a.fp8 else None,
             "fp8_fused_epilogues": bool(a.fp8_fused_epi) if a.fp8 else None,
             "fp8_keep_fused": a.fp8_keep_fused if a.fp8 else None,
