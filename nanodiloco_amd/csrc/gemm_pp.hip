@@ -210,7 +210,8 @@ __device__ __forceinline__ void pp_epilogue(const f32x4 (&acc)[8][4], bf16_t* __
   // store cache policy: nt (aux 2) by default, plain with ABL 32; ABL 2048 adds sc1 (aux 16), whose stores do not
   // keep the written line in the XCD's L2 (MI355X_MICROARCH store flavours) -- A/B of L2 room for the K-loop
   constexpr int STP = ((ABL & 32) ? 0 : 2) | ((ABL & 2048) ? 16 : 0);
-  constexpr int SWP = (ABL & 2048) ? 16 : 0;  // the SwiGLU forward's direct stores (plain policy by default)
+  // the SwiGLU forward's direct (half-line) stores: plain policy by default; ABL 512 (A/B) nt like the staged ones
+  constexpr int SWP = ((ABL & 2048) ? 16 : 0) | ((ABL & 512) ? 2 : 0);
 
     // per-lane row offsets derive from an opaque zero: otherwise LICM hoists every row's store
     // offset out of the tile loop and keeps ~16 VGPRs live through the whole K-loop (spills)
@@ -820,13 +821,13 @@ int num_cus_pp() {
 
 // A/B builds: nd_gemm_pp_set_variant or ND_GEMM_PP_VARIANT (read once at load).  The product library
 // accepts only the correct-result variants (0 default, 32 plain-policy stores, 256 direct stores, 288 both,
-// 1024 buffer-form pieces, 2048 / 2080 sc1 nt / sc1 stores); the timing-only ablations with wrong results (1-16, 64, 128 and their sums)
+// 512 nt SwiGLU-forward stores, 1024 buffer-form pieces, 2048 / 2080 sc1 nt / sc1 stores); the timing-only ablations with wrong results (1-16, 64, 128 and their sums)
 // exist only in a -DND_ABLATION build (csrc/build.py --ablation -> _lib/alt/).
 bool pp_variant_ok(int v) {
 #ifdef ND_ABLATION
   return v >= 0;
 #else
-  return v == 0 || v == 32 || v == 256 || v == 288 || v == 1024 || v == 2048 || v == 2080;
+  return v == 0 || v == 32 || v == 256 || v == 288 || v == 512 || v == 1024 || v == 2048 || v == 2080;
 #endif
 }
 int g_pp_variant = [] {
@@ -855,6 +856,8 @@ template <int EPI, int HD = 64>
 int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
               const PPEpi& ep, hipStream_t s) {
   if (g_pp_variant == 1024) return launch_pp_v<EPI, HD, 1024>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+  if constexpr (EPI == PP_SWIGLU)
+    if (g_pp_variant == 512) return launch_pp_v<EPI, HD, 512>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);  // nt SwiGLU stores
   if (g_pp_variant == 2048) return launch_pp_v<EPI, HD, 2048>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);  // sc1 nt stores
   if (g_pp_variant == 2080) return launch_pp_v<EPI, HD, 2080>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);  // sc1 stores
 #ifdef ND_ABLATION
@@ -934,6 +937,8 @@ int launch_mlp(const void* A, const void* B, void* C, int M, int N, int K, int64
                const PPEpi& ep, hipStream_t s) {
   if (g_mlp_coef) {
     if constexpr (F8 == 0) {  // the store-policy A/B variants (bf16 only)
+      if (EPI == PP_SWIGLU && g_pp_variant == 512)
+        return launch_pp_v<PP_SWIGLU, 64, 512, 0, 0, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       if (g_pp_variant == 2048) return launch_pp_v<EPI, 64, 2048, 0, 0, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
       if (g_pp_variant == 2080) return launch_pp_v<EPI, 64, 2080, 0, 0, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
     }

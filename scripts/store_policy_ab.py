@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """In-process A/B of the ping-pong GEMM's C-store cache policy (ND_GEMM_PP_VARIANT / ops.gemm.set_pp_variant:
-0 nt stores, 2048 sc1 + nt, 2080 sc1 -- sc1 stores do not keep the written lines in the XCD's L2): the plain
+0 nt stores, 2048 sc1 + nt, 2080 sc1 -- sc1 stores do not keep the written lines in the XCD's L2; 512 nt for the
+SwiGLU forward's direct stores; VARIANTS=0,512 picks the arms): the plain
 Llama-150M products at 131,072 tokens on the own kernel and the three fused-epilogue products, interleaved,
 median of 5 rounds.
 
@@ -47,7 +48,7 @@ def main():
         "qkv+rope": lambda: G.gemm_pp_rope(x, wqkv, cos, sin, 1024, 64, 2 * d),
         "gu+swiglu": lambda: G.gemm_pp_swiglu(x, wgu), "down dgrad+dswiglu": lambda: G.gemm_pp_dswiglu(x, wdT, gu),
     }
-    variants = (0, 2048, 2080)
+    variants = tuple(int(v) for v in os.environ.get("VARIANTS", "0,2048,2080").split(","))
     for k in ("o fwd", "qkv+rope", "gu+swiglu", "down dgrad+dswiglu"):  # the policy must not change a bit
         outs = []
         for v in variants:

@@ -41,7 +41,7 @@ def test_default_library_has_no_ablation_instantiation():
             elif name == "attn_bwd_dkdv_dma_kernel" and len(t) >= 6:
                 assert t[5] == "0", ln
             elif name == "gemm_pp_kernel":
-                assert t[2] in ("0", "32", "256", "288", "1024", "2048", "2080"), ln  # 2048 / 2080: sc1 store policy
+                assert t[2] in ("0", "32", "256", "288", "512", "1024", "2048", "2080"), ln  # 512 / 2048 / 2080: store policy
             elif name == "gemm_w128_kernel":
                 assert t[3] == "0", ln
             elif name == "wgrad_pp_kernel" and len(t) >= 2:
