@@ -2,7 +2,7 @@
 # round 6 session 28: final validation at HEAD -- the whole GPU suite, smoke(), the default bench and --fp8
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r6final
+O=gpurun_out/r6final2
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
